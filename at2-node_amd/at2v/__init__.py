@@ -1,0 +1,245 @@
+"""at2v — Python binding (ctypes) of libat2v.so, the MI355X batch Ed25519 verifier.
+
+Thin plumbing over the C ABI in include/at2v.h, used by the tests and bench.py. The product is the
+HIP library. This module has NO CPU fallback: if libat2v.so or a gfx950 device is missing, every
+call raises.
+
+Reference interface mirrored (drop::crypto::sign, used by at2-node at src/lib.rs:5,19,
+src/client.rs:72-78, src/bin/server/rpc.rs:269,281):
+  * ``Signature.verify(message, public_key)`` raises ``VerifyError`` on a bad signature, like
+    drop's ``Signature::verify(&self, &T, &PublicKey) -> Result<(), VerifyError>``;
+  * ``BatchVerifier.verify_batch(...)`` is the batch form the server ingest uses.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libat2v.so")
+
+POLICY_DALEK_V1 = 0
+POLICY_LIBSODIUM_1_0_18 = 1
+_POLICIES = {"dalek": POLICY_DALEK_V1, "dalek_v1": POLICY_DALEK_V1, "libsodium": POLICY_LIBSODIUM_1_0_18,
+             "libsodium_1_0_18": POLICY_LIBSODIUM_1_0_18, POLICY_DALEK_V1: POLICY_DALEK_V1,
+             POLICY_LIBSODIUM_1_0_18: POLICY_LIBSODIUM_1_0_18}
+
+# must match include/at2v.h (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = ("at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
+                    "at2v_verify_one", "at2v_strerror", "at2v_gen_records_device", "at2v_sign_batch",
+                    "at2v_get_info")
+
+
+class At2vError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        super().__init__(f"at2v error {code}: {strerror(code)}{(' (' + what + ')') if what else ''}")
+        self.code = code
+
+
+class VerifyError(Exception):
+    """Signature rejected (drop::crypto::sign::VerifyError)."""
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int)]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("num_gpus", ctypes.c_int), ("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
+                ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int), ("vgprs", ctypes.c_int)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libat2v.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise At2vError(-2, f"{path} not built; run `make -C at2-node_amd` or __graft_entry__.build()")
+    # One HIP runtime per process: torch bundles its own libamdhip64 (same SONAME as ROCm's). If torch is
+    # present it must be loaded first so libat2v.so binds to the same runtime and torch streams/pointers
+    # passed to the *_device entry points belong to the runtime that launches our kernels.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(path)
+    P, u8p, u32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32)
+    lib.at2v_create.argtypes = [ctypes.POINTER(_Opts), ctypes.POINTER(P)]
+    lib.at2v_create.restype = ctypes.c_int
+    lib.at2v_destroy.argtypes = [P]
+    lib.at2v_destroy.restype = None
+    lib.at2v_verify_batch.argtypes = [P, P, P, P, P, ctypes.c_size_t, P]
+    lib.at2v_verify_batch.restype = ctypes.c_int
+    lib.at2v_verify_batch_device.argtypes = [P, P, P, P, ctypes.c_size_t, P, ctypes.c_size_t, P, P]
+    lib.at2v_verify_batch_device.restype = ctypes.c_int
+    lib.at2v_verify_one.argtypes = [P, P, P, ctypes.c_size_t]
+    lib.at2v_verify_one.restype = ctypes.c_int
+    lib.at2v_strerror.argtypes = [ctypes.c_int]
+    lib.at2v_strerror.restype = ctypes.c_char_p
+    lib.at2v_gen_records_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
+                                            P, P, P, P, P]
+    lib.at2v_gen_records_device.restype = ctypes.c_int
+    lib.at2v_sign_batch.argtypes = [P, P, P, P, ctypes.c_size_t, P, P]
+    lib.at2v_sign_batch.restype = ctypes.c_int
+    lib.at2v_get_info.argtypes = [P, ctypes.POINTER(_Info)]
+    lib.at2v_get_info.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def strerror(code: int) -> str:
+    try:
+        return load_library().at2v_strerror(code).decode()
+    except At2vError:
+        return "library not loaded"
+
+
+def _check(rc: int, what: str = "") -> int:
+    if rc < 0:
+        raise At2vError(rc, what)
+    return rc
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def unpack_verdicts(words: np.ndarray, n: int) -> np.ndarray:
+    """verdict words (bit i%32 of word i/32) -> bool[n]"""
+    bits = np.unpackbits(np.ascontiguousarray(words, dtype="<u4").view(np.uint8), bitorder="little")
+    return bits[:n].astype(bool)
+
+
+def pack_records(pks: Sequence[bytes], sigs: Sequence[bytes], msgs: Sequence[bytes]):
+    """lists of bytes -> (pk[n,32], sig[n,64], msg u8[], off u32[n+1]) in the ABI layout"""
+    n = len(pks)
+    pk = np.frombuffer(b"".join(pks), dtype=np.uint8).reshape(n, 32) if n else np.zeros((0, 32), np.uint8)
+    sig = np.frombuffer(b"".join(sigs), dtype=np.uint8).reshape(n, 64) if n else np.zeros((0, 64), np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint32)
+    if n:
+        off[1:] = np.cumsum([len(m) for m in msgs])
+    msg = np.frombuffer(b"".join(msgs), dtype=np.uint8) if n else np.zeros(0, np.uint8)
+    return pk, sig, msg, off
+
+
+class BatchVerifier:
+    """Owns an at2v context (one or more gfx950 devices)."""
+
+    def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek"):
+        self._lib = load_library()
+        self.policy = _POLICIES[policy]
+        opts = _Opts(device, num_gpus, self.policy)
+        h = ctypes.c_void_p()
+        _check(self._lib.at2v_create(ctypes.byref(opts), ctypes.byref(h)), "at2v_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.at2v_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def info(self) -> dict:
+        inf = _Info()
+        _check(self._lib.at2v_get_info(self._h, ctypes.byref(inf)), "at2v_get_info")
+        return {f: getattr(inf, f) for f, _ in _Info._fields_}
+
+    def verify_batch(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, msg_off: np.ndarray) -> np.ndarray:
+        """host arrays -> bool[n] verdicts"""
+        pk = np.ascontiguousarray(pk, dtype=np.uint8)
+        sig = np.ascontiguousarray(sig, dtype=np.uint8)
+        msg = np.ascontiguousarray(msg, dtype=np.uint8).reshape(-1)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        n = len(msg_off) - 1
+        if pk.size != 32 * n or sig.size != 64 * n:
+            raise ValueError("pk/sig/msg_off sizes disagree")
+        words = np.zeros(max(1, (n + 31) // 32), dtype=np.uint32)
+        msg_arg = msg if msg.size else np.zeros(1, np.uint8)
+        _check(self._lib.at2v_verify_batch(self._h, _ptr(pk), _ptr(sig), _ptr(msg_arg), _ptr(msg_off), n,
+                                           _ptr(words)), "at2v_verify_batch")
+        return unpack_verdicts(words, n)
+
+    def verify_batch_device(self, d_pk: int, d_sig: int, d_msg: int, msg_bytes: int, d_off: int, n: int,
+                            d_verdicts: int, stream: int = 0) -> None:
+        """device pointers (e.g. torch tensor data_ptr()), asynchronous on `stream` (a hipStream_t)"""
+        _check(self._lib.at2v_verify_batch_device(self._h, d_pk, d_sig, d_msg, msg_bytes, d_off, n, d_verdicts,
+                                                  stream or None), "at2v_verify_batch_device")
+
+    def gen_records_device(self, cfg_seed: int, first: int, n: int, msg_len: int, d_pk: int, d_sig: int, d_msg: int,
+                           d_off: Optional[int], stream: int = 0) -> None:
+        _check(self._lib.at2v_gen_records_device(self._h, cfg_seed, first, n, msg_len, d_pk, d_sig, d_msg,
+                                                 d_off or None, stream or None), "at2v_gen_records_device")
+
+    def sign_batch(self, seeds: np.ndarray, msg: np.ndarray, msg_off: np.ndarray):
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+        msg = np.ascontiguousarray(msg, dtype=np.uint8).reshape(-1)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        n = len(msg_off) - 1
+        pk = np.zeros((n, 32), np.uint8)
+        sig = np.zeros((n, 64), np.uint8)
+        msg_arg = msg if msg.size else np.zeros(1, np.uint8)
+        _check(self._lib.at2v_sign_batch(self._h, _ptr(seeds), _ptr(msg_arg), _ptr(msg_off), n, _ptr(pk), _ptr(sig)),
+               "at2v_sign_batch")
+        return pk, sig
+
+
+def verify_one(pk: bytes, sig: bytes, msg: bytes) -> bool:
+    lib = load_library()
+    a = np.frombuffer(pk, np.uint8)
+    s = np.frombuffer(sig, np.uint8)
+    m = np.frombuffer(msg, np.uint8) if msg else np.zeros(1, np.uint8)
+    return bool(_check(lib.at2v_verify_one(_ptr(a), _ptr(s), _ptr(m), len(msg)), "at2v_verify_one"))
+
+
+# ------------------------------------------------ drop::crypto::sign mirror
+class PublicKey:
+    """32-byte Ed25519 public key (drop::crypto::sign::PublicKey). Decoding is checked by verify."""
+
+    def __init__(self, data: bytes):
+        if len(data) != 32:
+            raise ValueError("public key must be 32 bytes")
+        self.bytes = bytes(data)
+
+    def __bytes__(self):
+        return self.bytes
+
+    def __eq__(self, other):
+        return isinstance(other, PublicKey) and other.bytes == self.bytes
+
+    def __hash__(self):
+        return hash(self.bytes)
+
+    def __repr__(self):
+        return f"PublicKey({self.bytes.hex()})"
+
+
+class Signature:
+    """64-byte Ed25519 signature R || S (drop::crypto::sign::Signature)."""
+
+    def __init__(self, data: bytes):
+        if len(data) != 64:
+            raise ValueError("signature must be 64 bytes")
+        self.bytes = bytes(data)
+
+    def verify(self, message: bytes, public_key: PublicKey) -> None:
+        """Raise VerifyError unless the signature is valid (GPU path; no CPU fallback)."""
+        if not verify_one(public_key.bytes, self.bytes, bytes(message)):
+            raise VerifyError("signature verification failed")

@@ -1,0 +1,339 @@
+// at2v_api.hip — the C ABI of include/at2v.h (host side).
+//
+// A context owns, per device: a stream, the persistent-grid scratch for the per-lane A tables,
+// and growable device staging buffers for host batches. Host batches are split by index range
+// (aligned to 64 records = one wave chunk = two verdict words) across the context's devices;
+// each shard runs H2D -> verify -> D2H on its own stream, so shards overlap.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/at2v.h"
+
+namespace at2v {
+hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
+                         const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch, int grid,
+                         hipStream_t stream);
+hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint8_t* pk, uint8_t* sig,
+                      uint8_t* msg, uint32_t* off, hipStream_t stream);
+hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_total, const uint32_t* off, uint32_t n,
+                       uint8_t* pk, uint8_t* sig, hipStream_t stream);
+hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs);
+size_t scratch_bytes_per_block();
+int block_threads();
+}  // namespace at2v
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Shard {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int grid = 0;  // persistent grid (blocks)
+  int cus = 0;
+  int blocks_per_cu = 0;
+  int vgprs = 0;
+  DevBuf scratch, pk, sig, msg, off, verdict;
+};
+
+}  // namespace
+
+struct at2v_ctx {
+  at2v_policy policy = AT2V_POLICY_DALEK_V1;
+  std::vector<Shard> shards;
+};
+
+namespace {
+
+int hip_code(hipError_t e) {
+  if (e == hipSuccess) return AT2V_OK;
+  if (e == hipErrorOutOfMemory) return AT2V_E_OOM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorNoBinaryForGpu) return AT2V_E_NODEVICE;
+  return AT2V_E_HIP;
+}
+
+#define AT2V_TRY(expr)                       \
+  do {                                       \
+    hipError_t e_ = (expr);                  \
+    if (e_ != hipSuccess) return hip_code(e_); \
+  } while (0)
+
+int init_shard(Shard& s, int device) {
+  s.device = device;
+  AT2V_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  AT2V_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return AT2V_E_NODEVICE;
+  s.cus = prop.multiProcessorCount;
+  AT2V_TRY(at2v::verify_occupancy(&s.blocks_per_cu, &s.vgprs));
+  if (s.blocks_per_cu < 1) s.blocks_per_cu = 1;
+  s.grid = s.cus * s.blocks_per_cu;
+  AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  AT2V_TRY(s.scratch.ensure((size_t)s.grid * at2v::scratch_bytes_per_block()));
+  return AT2V_OK;
+}
+
+bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
+  if (!out) return AT2V_E_INVALID;
+  *out = nullptr;
+  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1};
+  if (opts) o = *opts;
+  if (o.num_gpus <= 0) o.num_gpus = 1;
+  if (o.policy != AT2V_POLICY_DALEK_V1 && o.policy != AT2V_POLICY_LIBSODIUM_1_0_18) return AT2V_E_INVALID;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return AT2V_E_NODEVICE;
+  if (o.device < 0 || o.device + o.num_gpus > ndev) return AT2V_E_NODEVICE;
+  at2v_ctx* c = new (std::nothrow) at2v_ctx;
+  if (!c) return AT2V_E_OOM;
+  c->policy = o.policy;
+  c->shards.resize((size_t)o.num_gpus);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int g = 0; g < o.num_gpus; ++g) {
+    int rc = init_shard(c->shards[(size_t)g], o.device + g);
+    if (rc != AT2V_OK) {
+      (void)hipSetDevice(prev);
+      at2v_destroy(c);
+      return rc;
+    }
+  }
+  (void)hipSetDevice(prev);
+  *out = c;
+  return AT2V_OK;
+}
+
+void at2v_destroy(at2v_ctx* ctx) {
+  if (!ctx) return;
+  for (Shard& s : ctx->shards) {
+    if (hipSetDevice(s.device) != hipSuccess) continue;
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    s.scratch.release();
+    s.pk.release();
+    s.sig.release();
+    s.msg.release();
+    s.off.release();
+    s.verdict.release();
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  delete ctx;
+}
+
+int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                      const uint32_t* msg_off, size_t n, uint32_t* verdicts) {
+  if (!ctx) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!pk || !sig || !msg_off || !verdicts || n >= (1u << 31)) return AT2V_E_INVALID;
+  if (!msg && msg_off[n] != msg_off[0]) return AT2V_E_INVALID;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  const size_t G = ctx->shards.size();
+  // shard boundaries aligned to 64 records
+  std::vector<size_t> lo(G + 1);
+  const size_t chunks = (n + 63) / 64;
+  for (size_t g = 0; g <= G; ++g) lo[g] = std::min(n, (chunks * g / G) * 64);
+  int rc = AT2V_OK;
+  std::vector<std::vector<uint32_t>> offs_all(G);  // must outlive the async uploads
+  for (size_t g = 0; g < G && rc == AT2V_OK; ++g) {
+    Shard& s = ctx->shards[g];
+    const size_t a = lo[g], b = lo[g + 1], m = b - a;
+    if (m == 0) continue;
+    hipError_t e = hipSetDevice(s.device);
+    const uint32_t mb0 = msg_off[a], mb1 = msg_off[b];
+    if (mb1 < mb0) {
+      rc = AT2V_E_INVALID;
+      break;
+    }
+    const size_t mbytes = (size_t)(mb1 - mb0);
+    if (e == hipSuccess) e = s.pk.ensure(m * 32);
+    if (e == hipSuccess) e = s.sig.ensure(m * 64);
+    if (e == hipSuccess) e = s.msg.ensure(mbytes + 16);
+    if (e == hipSuccess) e = s.off.ensure((m + 1) * 4);
+    if (e == hipSuccess) e = s.verdict.ensure(((m + 31) / 32) * 4);
+    // offsets rebased to the shard's message slice
+    std::vector<uint32_t>& offs = offs_all[g];
+    offs.resize(m + 1);
+    for (size_t i = 0; i <= m; ++i) {
+      offs[i] = msg_off[a + i] - mb0;
+      if (i && offs[i] < offs[i - 1]) rc = AT2V_E_INVALID;
+    }
+    if (rc != AT2V_OK) break;
+    if (e == hipSuccess) e = hipMemcpyAsync(s.pk.p, pk + a * 32, m * 32, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.sig.p, sig + a * 64, m * 64, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess && mbytes)
+      e = hipMemcpyAsync(s.msg.p, msg + mb0, mbytes, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.off.p, offs.data(), (m + 1) * 4, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = at2v::launch_verify((const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
+                              (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (int)ctx->policy,
+                              (uint32_t*)s.verdict.p, (int4*)s.scratch.p, s.grid, s.stream);
+    // a = multiple of 64 => the shard's words start at word a/32
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(verdicts + a / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, s.stream);
+    if (e != hipSuccess) rc = hip_code(e);
+  }
+  // shards run concurrently on their own devices/streams; wait for all of them
+  for (size_t g = 0; g < G; ++g) {
+    Shard& s = ctx->shards[g];
+    if (hipSetDevice(s.device) != hipSuccess) continue;
+    hipError_t e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
+  }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                             size_t msg_bytes, const uint32_t* d_msg_off, size_t n, uint32_t* d_verdicts,
+                             void* hip_stream) {
+  if (!ctx) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!d_pk || !d_sig || !d_msg_off || !d_verdicts || n >= (1u << 31) || msg_bytes >= (1ull << 32))
+    return AT2V_E_INVALID;
+  if (!aligned(d_pk, 16) || !aligned(d_sig, 16) || !aligned(d_msg_off, 4) || !aligned(d_verdicts, 4))
+    return AT2V_E_ALIGN;
+  Shard& s = ctx->shards[0];
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(s.device);
+  if (e == hipSuccess)
+    e = at2v::launch_verify(d_pk, d_sig, d_msg, (uint32_t)msg_bytes, d_msg_off, (uint32_t)n, (int)ctx->policy,
+                            d_verdicts, (int4*)s.scratch.p, s.grid, (hipStream_t)hip_stream);
+  (void)hipSetDevice(prev);
+  return hip_code(e);
+}
+
+static std::mutex g_one_mu;
+static at2v_ctx* g_one_ctx = nullptr;
+
+int at2v_verify_one(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len) {
+  if (!pk || !sig || (!msg && len) || len >= (1ull << 31)) return AT2V_E_INVALID;
+  std::lock_guard<std::mutex> lk(g_one_mu);
+  if (!g_one_ctx) {
+    int rc = at2v_create(nullptr, &g_one_ctx);
+    if (rc != AT2V_OK) {
+      g_one_ctx = nullptr;
+      return rc;
+    }
+  }
+  uint32_t off[2] = {0, (uint32_t)len};
+  uint32_t verdict = 0;
+  static const uint8_t empty[1] = {0};
+  int rc = at2v_verify_batch(g_one_ctx, pk, sig, len ? msg : empty, off, 1, &verdict);
+  return rc < 0 ? rc : (int)(verdict & 1u);
+}
+
+const char* at2v_strerror(int code) {
+  switch (code) {
+    case AT2V_OK: return "ok";
+    case AT2V_E_INVALID: return "invalid argument";
+    case AT2V_E_NODEVICE: return "no usable gfx950 device";
+    case AT2V_E_HIP: return "HIP runtime error";
+    case AT2V_E_OOM: return "out of memory";
+    case AT2V_E_ALIGN: return "misaligned device pointer";
+    case AT2V_E_RCCL: return "RCCL error";
+    default: return "unknown error";
+  }
+}
+
+int at2v_gen_records_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
+                            uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg, uint32_t* d_msg_off, void* hip_stream) {
+  if (!ctx) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!d_pk || !d_sig || (!d_msg && msg_len) || n >= (1u << 31) || (uint64_t)n * msg_len >= (1ull << 32))
+    return AT2V_E_INVALID;
+  if (!aligned(d_pk, 4) || !aligned(d_sig, 4) || (d_msg_off && !aligned(d_msg_off, 4))) return AT2V_E_ALIGN;
+  Shard& s = ctx->shards[0];
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(s.device);
+  if (e == hipSuccess)
+    e = at2v::launch_gen(cfg_seed, first, (uint32_t)n, msg_len, d_pk, d_sig, d_msg, d_msg_off,
+                         (hipStream_t)hip_stream);
+  (void)hipSetDevice(prev);
+  return hip_code(e);
+}
+
+int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, const uint32_t* msg_off, size_t n,
+                    uint8_t* pk_out, uint8_t* sig_out) {
+  if (!ctx) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!seeds || !msg_off || !pk_out || !sig_out || n >= (1u << 31)) return AT2V_E_INVALID;
+  Shard& s = ctx->shards[0];
+  const uint32_t mb0 = msg_off[0], mb1 = msg_off[n];
+  if (mb1 < mb0 || (!msg && mb1 != mb0)) return AT2V_E_INVALID;
+  const size_t mbytes = mb1 - mb0;
+  std::vector<uint32_t> offs(n + 1);
+  for (size_t i = 0; i <= n; ++i) {
+    offs[i] = msg_off[i] - mb0;
+    if (i && offs[i] < offs[i - 1]) return AT2V_E_INVALID;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  DevBuf dseed, dmsg, doff, dpk, dsig;
+  hipError_t e = hipSetDevice(s.device);
+  if (e == hipSuccess) e = dseed.ensure(n * 32);
+  if (e == hipSuccess) e = dmsg.ensure(mbytes + 16);
+  if (e == hipSuccess) e = doff.ensure((n + 1) * 4);
+  if (e == hipSuccess) e = dpk.ensure(n * 32);
+  if (e == hipSuccess) e = dsig.ensure(n * 64);
+  if (e == hipSuccess) e = hipMemcpyAsync(dseed.p, seeds, n * 32, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess && mbytes) e = hipMemcpyAsync(dmsg.p, msg + mb0, mbytes, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(doff.p, offs.data(), (n + 1) * 4, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess)
+    e = at2v::launch_sign((const uint8_t*)dseed.p, (const uint8_t*)dmsg.p, (uint32_t)mbytes, (const uint32_t*)doff.p,
+                          (uint32_t)n, (uint8_t*)dpk.p, (uint8_t*)dsig.p, s.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(pk_out, dpk.p, n * 32, hipMemcpyDeviceToHost, s.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(sig_out, dsig.p, n * 64, hipMemcpyDeviceToHost, s.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+  dseed.release();
+  dmsg.release();
+  doff.release();
+  dpk.release();
+  dsig.release();
+  (void)hipSetDevice(prev);
+  return hip_code(e);
+}
+
+int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
+  if (!ctx || !out || ctx->shards.empty()) return AT2V_E_INVALID;
+  const Shard& s = ctx->shards[0];
+  out->num_gpus = (int)ctx->shards.size();
+  out->grid_blocks = s.grid;
+  out->block_threads = at2v::block_threads();
+  out->waves_per_cu = s.blocks_per_cu * at2v::block_threads() / 64;
+  out->cus = s.cus;
+  out->vgprs = s.vgprs;
+  return AT2V_OK;
+}
+
+}  // extern "C"

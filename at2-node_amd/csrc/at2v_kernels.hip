@@ -1,0 +1,383 @@
+// at2v_kernels.hip — gfx950 kernels: batch verify (the hot path) and the GPU record generator / signer.
+//
+// Verify kernel layout:
+//   * one lane = one signature; a wave owns a contiguous chunk of 64 records, so the verdict bits of a
+//     chunk are one __ballot -> two uint32 words written by lane 0 (no atomics, no cross-wave traffic);
+//   * persistent grid (resident waves only), chunk = wave_id + k * total_waves; each wave reuses a fixed
+//     92 KiB slice of the scratch buffer for its 64 per-lane tables [0..8](-A) (cached form, 160 B each),
+//     lane-interleaved in 16-byte granules so a table store is one coalesced 1 KiB row per granule;
+//   * the fixed-base table [0..128]B (affine Niels, 128 B per entry) is staged once per workgroup in LDS;
+//   * records are read straight from the ABI layout (pk n x 32, sig n x 64, msg + offsets) with
+//     16-byte loads for A/R/S and 4-byte loads + v_alignbit for unaligned message words.
+#include <hip/hip_runtime.h>
+
+#include "at2v_verify.h"
+
+namespace at2v {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kTabAGranules = 9 * 10;  // 9 entries x 10 x 16 B
+constexpr size_t kScratchPerWave = (size_t)kTabAGranules * 64 * 16;
+
+struct DevTabA {
+  int4* base;  // this wave's slice
+  int lane;
+  __device__ AT2V_INLINE void store(int e, const ge_cached& c) const {
+    const int32_t* w = reinterpret_cast<const int32_t*>(&c);
+#pragma unroll
+    for (int q = 0; q < 10; ++q)
+      base[(e * 10 + q) * 64 + lane] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+  __device__ AT2V_INLINE void load(int e, ge_cached& c) const {
+    int32_t* w = reinterpret_cast<int32_t*>(&c);
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const int4 v = base[(e * 10 + q) * 64 + lane];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+  }
+};
+
+struct LdsTabB {
+  const int4* lds;  // AT2V_BTAB_ENTRIES x 8 granules
+  __device__ AT2V_INLINE void load(int e, ge_niels& n) const {
+    int32_t w[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int4 v = lds[e * 8 + q];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      n.ypx.v[k] = w[k];
+      n.ymx.v[k] = w[10 + k];
+      n.xy2d.v[k] = w[20 + k];
+    }
+  }
+};
+
+__device__ AT2V_INLINE void stage_btab(int4* lds) {
+  const int4* src = reinterpret_cast<const int4*>(AT2V_BTAB);
+  for (int i = threadIdx.x; i < AT2V_BTAB_ENTRIES * 8; i += blockDim.x) lds[i] = src[i];
+  __syncthreads();
+}
+
+__device__ AT2V_INLINE void load8(uint32_t w[8], const uint8_t* p) {  // 32 bytes, 16-B aligned
+  const uint4 a = reinterpret_cast<const uint4*>(p)[0];
+  const uint4 b = reinterpret_cast<const uint4*>(p)[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// little-endian 32-bit word at byte address a of a buffer of `total` bytes; bytes >= total read as 0
+__device__ AT2V_INLINE uint32_t load_u32_guarded(const uint8_t* buf, uint32_t a, uint32_t total) {
+  if (a + 4 <= total) return *reinterpret_cast<const uint32_t*>(buf + a);
+  uint32_t v = 0;
+  for (uint32_t b = 0; b < 4; ++b)
+    if (a + b < total) v |= (uint32_t)buf[a + b] << (8 * b);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void verify_kernel(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                        const uint8_t* __restrict__ msg, uint32_t msg_total,
+                                                        const uint32_t* __restrict__ off, uint32_t n, int policy,
+                                                        uint32_t* __restrict__ verdicts, int4* __restrict__ scratch) {
+  __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+  stage_btab(btab);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t nchunks = (n + 63) / 64;
+  const uint32_t nwords = (n + 31) / 32;
+  DevTabA ta{scratch + (size_t)wave * (kTabAGranules * 64), lane};
+  LdsTabB tb{btab};
+  for (uint32_t chunk = wave; chunk < nchunks; chunk += nwaves) {
+    const uint32_t i = chunk * 64 + lane;
+    const bool live = i < n;
+    const uint32_t ii = live ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
+    uint32_t Rw[8], Sw[8], Aw[8];
+    load8(Rw, sig + (size_t)ii * 64);
+    load8(Sw, sig + (size_t)ii * 64 + 32);
+    load8(Aw, pk + (size_t)ii * 32);
+    const uint32_t o0 = off[ii];
+    const uint32_t len = off[ii + 1] - o0;
+    auto msgword = [&](uint32_t j) -> uint32_t {
+      const uint32_t a = o0 + 4 * j;
+      const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+      const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+      if (sh == 0) return lo;
+      const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+      return __builtin_amdgcn_alignbit(hi, lo, sh);
+    };
+    int ok = verify_core(Rw, Aw, Sw, len, msgword, policy, ta, tb);
+    ok &= live;
+    const uint64_t mask = __ballot(ok);
+    if (lane == 0) {
+      verdicts[2 * chunk] = (uint32_t)mask;
+      if (2 * chunk + 1 < nwords) verdicts[2 * chunk + 1] = (uint32_t)(mask >> 32);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ signing side
+
+// [s]B for a reduced scalar s < l: Horner over 32 signed radix-256 digits, 8 doublings per digit
+template <class TabB>
+__device__ AT2V_INLINE void ge_scalarmult_base(ge_p2& out, const uint32_t s[8], const TabB& tb) {
+  uint32_t sd[8];
+  sc_recode8(sd, s);
+  ge_p3 R3;
+  ge_p1p1 t;
+  ge_niels nb;
+  ge_p3_identity(R3);
+  ge_p2 R2;
+  for (int j = 31; j >= 0; --j) {
+    if (j != 31) {
+      for (int r = 0; r < 7; ++r) {
+        ge_p2_dbl(t, R2);
+        ge_p1p1_to_p2(R2, t);
+      }
+      ge_p2_dbl(t, R2);
+      ge_p1p1_to_p3(R3, t);
+    }
+    const int e = (int)((sd[j >> 2] >> (8 * (j & 3))) & 255) - 128;
+    tb.load(e < 0 ? -e : e, nb);
+    ge_niels_cneg(nb, e < 0);
+    ge_madd(t, R3, nb);
+    ge_p1p1_to_p2(R2, t);
+  }
+  out = R2;
+}
+
+__device__ AT2V_INLINE void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]) {
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t t = (uint64_t)a[i] * b[j] + x[i + j] + carry;
+      x[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    x[i + 8] = (uint32_t)carry;
+  }
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint64_t t = (uint64_t)x[i] + (i < 8 ? c[i] : 0u) + carry;
+    x[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  sc_reduce512(out, x);  // a, b, c < 2^253 so the sum < 2^507
+}
+
+// RFC 8032 sign of M under `seed` (8 LE words); writes pk (8 words) and R||S (16 words)
+template <class TabB, class MsgWord>
+__device__ AT2V_INLINE void sign_core(uint32_t pkw[8], uint32_t sigw[16], const uint32_t seed[8], uint32_t len,
+                                      MsgWord msgword, const TabB& tb) {
+  uint64_t h[8];
+  uint32_t hw[16];
+  sha512_prefixed<8>(h, seed, 0, [](uint32_t) { return 0u; });
+  sha512_digest_words(hw, h);
+  uint32_t a[8], prefix[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a[i] = hw[i];
+    prefix[i] = hw[8 + i];
+  }
+  a[0] &= 0xfffffff8u;
+  a[7] = (a[7] & 0x7fffffffu) | 0x40000000u;
+  uint32_t a16[16], ared[8];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a16[i] = i < 8 ? a[i] : 0u;
+  sc_reduce512(ared, a16);
+  ge_p2 P;
+  ge_scalarmult_base(P, ared, tb);
+  ge_p2_tobytes(pkw, P);
+  // r = H(prefix || M) mod l ; R = [r]B
+  sha512_prefixed<8>(h, prefix, len, msgword);
+  sha512_digest_words(hw, h);
+  uint32_t r[8];
+  sc_reduce512(r, hw);
+  ge_scalarmult_base(P, r, tb);
+  ge_p2_tobytes(sigw, P);
+  // k = H(R || A || M) mod l ; S = r + k a mod l
+  uint32_t pre[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sigw[i];
+    pre[8 + i] = pkw[i];
+  }
+  sha512_prefixed<16>(h, pre, len, msgword);
+  sha512_digest_words(hw, h);
+  uint32_t k[8];
+  sc_reduce512(k, hw);
+  sc_muladd(sigw + 8, k, ared, r);
+}
+
+// SHA-512 of a short byte string held in registers as LE words (len <= 64)
+template <int NW>
+__device__ AT2V_INLINE void sha512_words(uint32_t out16[16], const uint32_t (&wds)[NW], uint32_t len) {
+  uint64_t h[8];
+  sha512_prefixed<0>(h, nullptr, len, [&](uint32_t j) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int m = 0; m < NW; ++m) v = (j == (uint32_t)m) ? wds[m] : v;
+    return v;
+  });
+  sha512_digest_words(out16, h);
+}
+
+// seed_i and M_i of the deterministic generator (byte strings "at2v/seed"||u64le||u64le, 25 bytes, and
+// "at2v/msg"||u64le cfg||u64le i||u64le ctr, 32 bytes)
+__device__ AT2V_INLINE void gen_seed(uint32_t seed[8], uint64_t cfg, uint64_t idx) {
+  // bytes: a t 2 v / s e e d | cfg(8) | idx(8)
+  uint32_t w[7];
+  w[0] = 0x76327461u;                                               // "at2v"
+  w[1] = 0x6565732fu;                                               // "/see"
+  w[2] = 0x64u | ((uint32_t)(cfg & 0xffffff) << 8);                 // "d" + cfg[0..2]
+  w[3] = (uint32_t)(cfg >> 24);                                     // cfg[3..6]
+  w[4] = (uint32_t)(cfg >> 56) | ((uint32_t)(idx & 0xffffff) << 8); // cfg[7] + idx[0..2]
+  w[5] = (uint32_t)(idx >> 24);                                     // idx[3..6]
+  w[6] = (uint32_t)(idx >> 56);                                     // idx[7]
+  uint32_t o[16];
+  sha512_words<7>(o, w, 25);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) seed[i] = o[i];
+}
+
+__device__ AT2V_INLINE void gen_msg_block(uint32_t out16[16], uint64_t cfg, uint64_t idx, uint64_t ctr) {
+  uint32_t w[8];
+  w[0] = 0x76327461u;  // "at2v"
+  w[1] = 0x67736d2fu;  // "/msg"
+  w[2] = (uint32_t)cfg;
+  w[3] = (uint32_t)(cfg >> 32);
+  w[4] = (uint32_t)idx;
+  w[5] = (uint32_t)(idx >> 32);
+  w[6] = (uint32_t)ctr;
+  w[7] = (uint32_t)(ctr >> 32);
+  sha512_words<8>(out16, w, 32);
+}
+
+__global__ __launch_bounds__(kBlock) void gen_kernel(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len,
+                                                     uint8_t* __restrict__ pk, uint8_t* __restrict__ sig,
+                                                     uint8_t* __restrict__ msg, uint32_t* __restrict__ off) {
+  __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+  stage_btab(btab);
+  LdsTabB tb{btab};
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t idx = first + i;
+  uint32_t seed[8];
+  gen_seed(seed, cfg, idx);
+  // message bytes into the output buffer (byte stores; msg_len arbitrary)
+  uint8_t* m = msg + (size_t)i * msg_len;
+  for (uint32_t ctr = 0; ctr * 64 < msg_len; ++ctr) {
+    uint32_t blk[16];
+    gen_msg_block(blk, cfg, idx, ctr);
+    for (uint32_t b = 0; b < 64 && ctr * 64 + b < msg_len; ++b) m[ctr * 64 + b] = (uint8_t)(blk[b >> 2] >> (8 * (b & 3)));
+  }
+  if (off) {
+    off[i] = i * msg_len;
+    if (i == n - 1) off[n] = n * msg_len;
+  }
+  const uint32_t mtotal = n * msg_len, o0 = i * msg_len;
+  auto msgword = [&](uint32_t j) -> uint32_t {  // this lane's own bytes, written just above
+    const uint32_t a = o0 + 4 * j;
+    const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+    const uint32_t lo = load_u32_guarded(msg, a0, mtotal);
+    if (sh == 0) return lo;
+    return __builtin_amdgcn_alignbit(load_u32_guarded(msg, a0 + 4, mtotal), lo, sh);
+  };
+  uint32_t pkw[8], sigw[16];
+  sign_core(pkw, sigw, seed, msg_len, msgword, tb);
+  uint32_t* pko = reinterpret_cast<uint32_t*>(pk + (size_t)i * 32);
+  uint32_t* sgo = reinterpret_cast<uint32_t*>(sig + (size_t)i * 64);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) pko[q] = pkw[q];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) sgo[q] = sigw[q];
+}
+
+__global__ __launch_bounds__(kBlock) void sign_kernel(const uint8_t* __restrict__ seeds, const uint8_t* __restrict__ msg,
+                                                      uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n,
+                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sig) {
+  __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+  stage_btab(btab);
+  LdsTabB tb{btab};
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t seed[8];
+  load8(seed, seeds + (size_t)i * 32);
+  const uint32_t o0 = off[i];
+  const uint32_t len = off[i + 1] - o0;
+  auto msgword = [&](uint32_t j) -> uint32_t {
+    const uint32_t a = o0 + 4 * j;
+    const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+    const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+    if (sh == 0) return lo;
+    return __builtin_amdgcn_alignbit(load_u32_guarded(msg, a0 + 4, msg_total), lo, sh);
+  };
+  uint32_t pkw[8], sigw[16];
+  sign_core(pkw, sigw, seed, len, msgword, tb);
+  uint32_t* pko = reinterpret_cast<uint32_t*>(pk + (size_t)i * 32);
+  uint32_t* sgo = reinterpret_cast<uint32_t*>(sig + (size_t)i * 64);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) pko[q] = pkw[q];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) sgo[q] = sigw[q];
+}
+
+// ------------------------------------------------------------------ launchers (host side)
+
+hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
+                         const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch, int grid,
+                         hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nchunks = (n + 63) / 64;
+  const uint32_t need_blocks = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
+  hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+                     verdicts, scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint8_t* pk, uint8_t* sig,
+                      uint8_t* msg, uint32_t* off, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gen_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, cfg, first, n, msg_len, pk,
+                     sig, msg, off);
+  return hipGetLastError();
+}
+
+hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_total, const uint32_t* off, uint32_t n,
+                       uint8_t* pk, uint8_t* sig, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(sign_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, seeds, msg, msg_total, off,
+                     n, pk, sig);
+  return hipGetLastError();
+}
+
+hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs) {
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, verify_kernel, kBlock, 0);
+  if (e != hipSuccess) return e;
+  hipFuncAttributes attr;
+  e = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(verify_kernel));
+  if (e == hipSuccess && vgprs) *vgprs = attr.numRegs;
+  return e;
+}
+
+size_t scratch_bytes_per_block() { return kScratchPerWave * kWavesPerBlock; }
+int block_threads() { return kBlock; }
+
+}  // namespace at2v

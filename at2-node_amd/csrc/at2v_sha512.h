@@ -1,0 +1,116 @@
+// at2v_sha512.h — SHA-512 (FIPS 180-4), one message per lane, for k = H(R || A || M) (SURVEY A V3)
+// and for the deterministic record generator / signer kernels.
+//
+// 64-bit words are emulated on the 32-bit VALU by the compiler (rotations -> v_alignbit_b32 pairs,
+// additions -> v_add_co/v_addc). The 80 rounds run as 5 rolled iterations of a 16-round unrolled
+// body whose message schedule lives in a 16-entry circular register window.
+#pragma once
+#include "at2v_fe_base.h"
+
+namespace at2v {
+
+AT2V_CONST_ARR uint64_t SHA512_K[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL, 0x3956c25bf348b538ULL,
+    0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL, 0xd807aa98a3030242ULL, 0x12835b0145706fbeULL,
+    0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL, 0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL,
+    0xc19bf174cf692694ULL, 0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL, 0x983e5152ee66dfabULL,
+    0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL, 0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL,
+    0x06ca6351e003826fULL, 0x142929670a0e6e70ULL, 0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL,
+    0x53380d139d95b3dfULL, 0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL, 0xd192e819d6ef5218ULL,
+    0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL, 0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL,
+    0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL, 0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL,
+    0x682e6ff3d6b2b8a3ULL, 0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL, 0xca273eceea26619cULL,
+    0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL, 0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL,
+    0x113f9804bef90daeULL, 0x1b710b35131c471bULL, 0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL,
+    0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+AT2V_HD AT2V_INLINE uint64_t sha_ror(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+AT2V_HD AT2V_INLINE uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+AT2V_HD AT2V_INLINE void sha512_init(uint64_t h[8]) {
+  h[0] = 0x6a09e667f3bcc908ULL; h[1] = 0xbb67ae8584caa73bULL; h[2] = 0x3c6ef372fe94f82bULL;
+  h[3] = 0xa54ff53a5f1d36f1ULL; h[4] = 0x510e527fade682d1ULL; h[5] = 0x9b05688c2b3e6c1fULL;
+  h[6] = 0x1f83d9abfb41bd6bULL; h[7] = 0x5be0cd19137e2179ULL;
+}
+
+// one compression; w[16] = the block as big-endian 64-bit words (clobbered)
+AT2V_HD AT2V_INLINE void sha512_compress(uint64_t h[8], uint64_t w[16]) {
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int r = 0; r < 80; r += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (r > 0) {
+        const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+        const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
+        w[i] += s0 + w[(i + 9) & 15] + s1;
+      }
+      const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
+      const uint64_t ch = (e & f) ^ (~e & g);
+      const uint64_t t1 = hh + S1 + ch + SHA512_K[r + i] + w[i];
+      const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
+      const uint64_t mj = (a & b) ^ (c & (a ^ b));
+      const uint64_t t2 = S0 + mj;
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// digest -> 16 little-endian 32-bit words of the 64-byte output (as bytes: big-endian h[0..7])
+AT2V_HD AT2V_INLINE void sha512_digest_words(uint32_t out[16], const uint64_t h[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    out[2 * i] = bswap32((uint32_t)(h[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)h[i]);
+  }
+}
+
+// SHA-512 of (prefix || M) where prefix is np 32-byte-word chunks given as LE words (np*8 words,
+// np in {0,1,2}) and M is read through `msgword(j)` = the j-th little-endian 32-bit word of M
+// (bytes 4j..4j+3; bytes past len may be garbage — they are masked here). len < 2^32.
+template <int NPW, class MsgWord>
+AT2V_HD AT2V_INLINE void sha512_prefixed(uint64_t h[8], const uint32_t* prefix, uint32_t len, MsgWord msgword) {
+  sha512_init(h);
+  const uint32_t total = (uint32_t)(4 * NPW) + len;                 // bytes hashed
+  const uint32_t nblocks = (total + 17 + 127) >> 7;
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      uint32_t be[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const uint32_t pos = (b << 7) + 8 * t + 4 * half;  // stream byte position (4-aligned)
+        uint32_t le;
+        if (pos < (uint32_t)(4 * NPW)) {
+          le = prefix[pos >> 2];
+        } else {
+          const uint32_t mo = pos - 4 * NPW;                 // message byte offset
+          uint32_t v = 0;
+          if (mo < len) v = msgword(mo >> 2);
+          const uint32_t nvalid = mo >= len ? 0u : (len - mo >= 4 ? 4u : len - mo);
+          if (nvalid < 4) {
+            v = nvalid ? (v & ((1u << (8 * nvalid)) - 1)) : 0u;
+            if (mo <= len) v |= 0x80u << (8 * nvalid);        // the 0x80 pad byte lands at mo + nvalid == len
+          }
+          le = v;
+        }
+        be[half] = bswap32(le);
+      }
+      w[t] = ((uint64_t)be[0] << 32) | be[1];
+    }
+    if (b == nblocks - 1) {
+      w[14] = 0;
+      w[15] = (uint64_t)total * 8;
+    }
+    sha512_compress(h, w);
+  }
+}
+
+}  // namespace at2v

@@ -1,0 +1,148 @@
+// at2v_verify.h — per-lane Ed25519 verify, dalek-1.x semantics (SURVEY.md Appendix A V1–V6).
+//
+// Replaces, per record, the call drop::crypto::sign → ed25519-dalek `PublicKey::verify` that
+// sieve/murmur make on every payload broadcast at /root/reference/src/bin/server/rpc.rs:275-284
+// (consumed already-verified at rpc.rs:156-173).
+//
+// Double-scalar multiplication R' = [k](-A) + [s]B uses one shared doubling chain with
+// wavefront-uniform fixed windows (every lane adds at the same positions, no divergence):
+//   k : 64 signed radix-16 digits  in [-8, 8]     -> table [0..8](-A), cached form, per lane (global scratch)
+//   s : 32 signed radix-256 digits in [-128, 128] -> table [0..128]B, affine Niels, in LDS
+//   R = sum_i 16^i (k_i(-A) + [i even] s_{i/2} B), Horner from i = 63: 252 doublings, 64 + 32 additions.
+// Any correct evaluation of [k](-A) + [s]B yields the same group element, so verdicts are
+// identical to dalek's NAF-5/NAF-8 vartime ladder (the oracle restates that one).
+#pragma once
+#include "at2v_ge.h"
+#include "at2v_sc.h"
+#include "at2v_sha512.h"
+
+namespace at2v {
+
+enum { POLICY_DALEK_V1 = 0, POLICY_LIBSODIUM_1_0_18 = 1 };
+
+// uniform-index select from an 8-word register array (avoids scratch for a runtime index)
+AT2V_HD AT2V_INLINE uint32_t sel8(const uint32_t w[8], int j) {
+  uint32_t r = w[0];
+#pragma unroll
+  for (int m = 1; m < 8; ++m) r = (j == m) ? w[m] : r;
+  return r;
+}
+
+// y-encoding (sign bit ignored) is canonical, i.e. y < p (libsodium ge25519_is_canonical)
+AT2V_HD AT2V_INLINE int enc_y_canonical(const uint32_t s[8]) {
+  const uint32_t top = s[7] & 0x7fffffffu;
+  const int hi_all = (top == 0x7fffffffu) & (s[6] == 0xffffffffu) & (s[5] == 0xffffffffu) & (s[4] == 0xffffffffu) &
+                     (s[3] == 0xffffffffu) & (s[2] == 0xffffffffu) & (s[1] == 0xffffffffu);
+  return !(hi_all & (s[0] >= 0xffffffedu));
+}
+
+// y-encoding (sign bit masked) is in libsodium 1.0.18's small-order blocklist
+AT2V_HD AT2V_INLINE int enc_small_order(const uint32_t s[8]) {
+  int hit = 0;
+#pragma unroll
+  for (int b = 0; b < 7; ++b) {
+    int eq = 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) eq &= ((i == 7 ? (s[i] & 0x7fffffffu) : s[i]) == AT2V_SMALL_ORDER_Y[b][i]);
+    hit |= eq;
+  }
+  return hit;
+}
+
+// Table access policies.
+//   TabA: void store(int e, const ge_cached&); void load(int e, ge_cached&)   (per lane, e in 0..8)
+//   TabB: void load(int e, ge_niels&)                                          (shared, e in 0..128)
+template <class TabA, class TabB, class MsgWord>
+AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                    MsgWord msgword, int policy, TabA& ta, const TabB& tb) {
+  // V1: s < l
+  int ok = sc_is_canonical(Sw);
+  if (policy == POLICY_LIBSODIUM_1_0_18) {
+    ok &= !enc_small_order(Rw);
+    ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
+  }
+  // V2: decode A (dalek rules)
+  ge_p3 A;
+  ok &= ge_frombytes(A, Aw);
+  // V3: k = SHA-512(R || A || M) mod l
+  uint32_t k[8];
+  {
+    uint32_t pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = Rw[i];
+      pre[8 + i] = Aw[i];
+    }
+    uint64_t h[8];
+    sha512_prefixed<16>(h, pre, len, msgword);
+    uint32_t hw[16];
+    sha512_digest_words(hw, h);
+    sc_reduce512(k, hw);
+  }
+  uint32_t kd[8], sd[8];
+  sc_recode4(kd, k);
+  sc_recode8(sd, Sw);
+
+  // table [j](-A), j = 0..8
+  fe_neg(A.X, A.X);
+  fe_neg(A.T, A.T);
+  {
+    ge_cached c1, cj;
+    ge_cached_identity(cj);
+    ta.store(0, cj);
+    ge_p3_to_cached(c1, A);
+    ta.store(1, c1);
+    ge_p3 P = A;
+    for (int j = 2; j <= 8; ++j) {
+      ge_p1p1 t;
+      ge_add(t, P, c1);
+      ge_p1p1_to_p3(P, t);
+      ge_p3_to_cached(cj, P);
+      ta.store(j, cj);
+    }
+  }
+
+  // V4: shared doubling chain over 64 radix-16 windows
+  ge_p2 R2;
+  ge_p3 R3;
+  ge_p1p1 t;
+  ge_cached ca;
+  ge_niels nb;
+  {  // top window i = 63 (odd: no B digit)
+    const int d = (int)(kd[7] >> 28) - 8;
+    ge_p3_identity(R3);
+    ta.load(d < 0 ? -d : d, ca);
+    ge_cached_cneg(ca, d < 0);
+    ge_add(t, R3, ca);
+    ge_p1p1_to_p2(R2, t);
+  }
+  for (int i = 62; i >= 0; --i) {
+    const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
+    ta.load(d < 0 ? -d : d, ca);  // issued before the doublings: latency hidden behind them
+    for (int r = 0; r < 3; ++r) {
+      ge_p2_dbl(t, R2);
+      ge_p1p1_to_p2(R2, t);
+    }
+    ge_p2_dbl(t, R2);
+    ge_p1p1_to_p3(R3, t);
+    ge_cached_cneg(ca, d < 0);
+    ge_add(t, R3, ca);
+    if ((i & 1) == 0) {
+      const int e = (int)((sel8(sd, i >> 3) >> (8 * ((i >> 1) & 3))) & 255) - 128;
+      ge_p1p1_to_p3(R3, t);
+      tb.load(e < 0 ? -e : e, nb);
+      ge_niels_cneg(nb, e < 0);
+      ge_madd(t, R3, nb);
+    }
+    ge_p1p1_to_p2(R2, t);
+  }
+  // V5/V6: canonical encoding of R' == R bytes
+  uint32_t enc[8];
+  ge_p2_tobytes(enc, R2);
+  int eq = 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= enc[i] == Rw[i];
+  return ok & eq;
+}
+
+}  // namespace at2v

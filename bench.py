@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py — Ed25519 verifies/s of the at2v hot path on 1..8 MI355X (BASELINE.json metric).
+
+Workload (BASELINE config 2, weak-scaled): every rank verifies its own batch of `--records-per-gpu`
+(default 1,048,576) signed transfers with 100-byte messages, generated on the GPU by the deterministic
+RFC 8032 generator and resident in HBM before timing starts. One step = one verify
+launch over the rank's batch + (N > 1) one RCCL all-gather of the verdict bitmap words over xGMI.
+Config 3 (16M over 8 GPUs) = `--records-per-gpu 2097152` at N = 8.
+
+Output: one JSON line on rank 0 with the contract fields plus `roofline` (VALU-bound) and
+`cpu_baseline` (the oracle, multi-threaded on host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
+
+CFG_SEED = 0x4154325F
+# nominal algorithmic work per verify, 32-bit VALU lane-ops (10-limb schoolbook estimate)
+ALG_OPS_PER_VERIFY = 1.1e6
+# int32 VALU issue peak per GPU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md chip table);
+# v_mad_i64_i32 (the field-multiply instruction) issues at half this rate (profiles/r01_ubench_valu.txt)
+VALU_PEAK_OPS = 256 * 128 * 2.4e9
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--msg-len", type=int, default=100)
+    ap.add_argument("--policy", default="dalek")
+    ap.add_argument("--cpu-sample", type=int, default=32768, help="records for the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import at2v
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("run N>1 under torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n, L = args.records_per_gpu, args.msg_len
+    n = (n + 63) // 64 * 64
+    v = at2v.BatchVerifier(device=local, policy=args.policy)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    d_pk = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    d_sig = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    d_msg = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    words = n // 32
+    d_ver = torch.zeros(words, dtype=torch.int32, device=dev)
+    d_all = torch.zeros(words * world, dtype=torch.int32, device=dev) if world > 1 else None
+    # distinct records per rank (indices rank*n .. rank*n+n-1)
+    v.gen_records_device(CFG_SEED, rank * n, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                         d_off.data_ptr(), s)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                              d_ver.data_ptr(), s)
+        if world > 1:
+            dist.all_gather_into_tensor(d_all, d_ver)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.steps):
+        kev[k][0].record(stream)
+        v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                              d_ver.data_ptr(), s)
+        kev[k][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(d_all, d_ver)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps
+    t_dev = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_dev, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = t_dev.tolist()
+
+    # verdict check after the timed region: every generated record must be valid, on every rank
+    full = d_all if world > 1 else d_ver
+    match = float((full == -1).float().mean().item())
+    if world > 1:
+        mt = torch.tensor([match], dtype=torch.float64, device=dev)
+        dist.all_reduce(mt, op=dist.ReduceOp.MIN)
+        match = mt.item()
+
+    total = n * world * args.steps
+    value = total / elapsed
+    per_gpu_kernel_rate = n / (kernel_ms * 1e-3)
+    achieved = per_gpu_kernel_rate * ALG_OPS_PER_VERIFY / 1e12
+    info = v.info()
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "ed25519 verifies/sec (node)",
+            "value": value,
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (GPU RFC 8032 generator, distinct keys, all signatures valid)",
+            "config": {
+                "workload": "BASELINE config 2: 1M signed transfers per GPU (100-byte M), dalek-1.x verify"
+                if n == 1 << 20 else f"{n} signed transfers per GPU ({L}-byte M)",
+                "records_per_gpu": n,
+                "msg_len": L,
+                "policy": args.policy,
+                "parallelism": f"index-shard x{world}" + (" + RCCL all-gather of verdict words" if world > 1 else ""),
+            },
+            "verdict_match": match,
+            "kernel_ms": kernel_ms,
+            "kernel": {"grid_blocks": info["grid_blocks"], "block": info["block_threads"],
+                       "waves_per_cu": info["waves_per_cu"], "vgprs": info["vgprs"]},
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": VALU_PEAK_OPS / 1e12,
+                "unit": "Tops/s (int32 lane-ops)",
+                "frac": achieved * 1e12 / VALU_PEAK_OPS,
+                "traffic": None,
+                "alg_ops_per_verify": ALG_OPS_PER_VERIFY,
+                "alg_bytes_per_verify": 32 + 64 + L + 4,
+                "hbm_frac": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9 / HBM_PEAK_GBS,
+            },
+        }
+    if rank == 0 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(args, d_pk, d_sig, d_msg, n, L)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    v.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, d_pk, d_sig, d_msg, n, L):
+    """The oracle (C restatement of the dalek-1.x verify, `port`), pthreads over host cores, on a bounded
+    sample of the same records. Stand-in for the reference's rayon ed25519-dalek path (not buildable)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py
+
+    m = min(args.cpu_sample, n)
+    pk = d_pk[: m * 32].cpu().numpy().reshape(m, 32)
+    sig = d_sig[: m * 64].cpu().numpy().reshape(m, 64)
+    msg = d_msg[: m * L].cpu().numpy()
+    off = (np.arange(m + 1) * L).astype(np.uint32)
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    o = oracle_py.Oracle()
+    o.verify_batch(pk[:64], sig[:64], msg[: 64 * L], off[:65], 0, threads)  # warm
+    t0 = time.perf_counter()
+    ok = o.verify_batch(pk, sig, msg, off, 0, threads)
+    dt = time.perf_counter() - t0
+    return {"value": m / dt, "unit": "verifies/s", "cores": threads, "kind": "port",
+            "sample": f"{m} records of the benchmark batch (100-byte M), oracle/ed25519_oracle.c, {threads} threads, "
+                      f"{dt:.2f} s wall; all valid={bool(ok.all())}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,68 @@
+// verify_host.cpp — TEST ONLY: compiles the product's device headers (at2-node_amd/csrc/*.h) for the
+// host and checks verify_core against a golden fixture file. Never part of the shipped path.
+// usage: verify_host <fixture.bin>   -> prints "n mismatches_dalek mismatches_sodium"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "at2v_verify.h"
+
+using namespace at2v;
+
+struct HostTabA {
+  ge_cached e[9];
+  void store(int i, const ge_cached& c) { e[i] = c; }
+  void load(int i, ge_cached& c) const { c = e[i]; }
+};
+struct HostTabB {
+  void load(int i, ge_niels& n) const {
+    const int32_t* p = &AT2V_BTAB[i * AT2V_BTAB_WORDS];
+    for (int k = 0; k < 10; ++k) {
+      n.ypx.v[k] = p[k];
+      n.ymx.v[k] = p[10 + k];
+      n.xy2d.v[k] = p[20 + k];
+    }
+  }
+};
+
+static void words(uint32_t w[8], const uint8_t* b) {
+  for (int i = 0; i < 8; ++i) w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+
+int main(int argc, char** argv) {
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  uint32_t hdr[4];
+  if (fread(hdr, 4, 4, f) != 4) return 2;
+  size_t n = hdr[2], mb = hdr[3];
+  std::vector<uint8_t> pk(32 * n), sig(64 * n), msg(mb + 8), vd(n), vs(n), cls(n);
+  std::vector<uint32_t> off(n + 1);
+  size_t ok = fread(pk.data(), 32, n, f) + fread(sig.data(), 64, n, f) + fread(off.data(), 4, n + 1, f);
+  ok += fread(msg.data(), 1, mb, f) + fread(vd.data(), 1, n, f) + fread(vs.data(), 1, n, f) + fread(cls.data(), 1, n, f);
+  fclose(f);
+  (void)ok;
+  size_t bad_d = 0, bad_s = 0;
+  int limit = argc > 2 ? atoi(argv[2]) : (int)n;
+  for (size_t i = 0; i < n && (int)i < limit; ++i) {
+    uint32_t R[8], A[8], S[8];
+    words(R, &sig[64 * i]);
+    words(S, &sig[64 * i + 32]);
+    words(A, &pk[32 * i]);
+    const uint8_t* m = &msg[off[i]];
+    uint32_t len = off[i + 1] - off[i];
+    auto mw = [&](uint32_t j) -> uint32_t {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; ++b) if (4 * j + b < len) v |= (uint32_t)m[4 * j + b] << (8 * b);
+      return v;
+    };
+    HostTabA ta;
+    HostTabB tb;
+    int d = verify_core(R, A, S, len, mw, POLICY_DALEK_V1, ta, tb);
+    int s = verify_core(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tb);
+    if (d != vd[i]) { if (bad_d < 10) fprintf(stderr, "dalek mismatch i=%zu cls=%d got=%d want=%d\n", i, cls[i], d, vd[i]); ++bad_d; }
+    if (s != vs[i]) { if (bad_s < 10) fprintf(stderr, "sodium mismatch i=%zu cls=%d got=%d want=%d\n", i, cls[i], s, vs[i]); ++bad_s; }
+  }
+  printf("%zu %zu %zu\n", n, bad_d, bad_s);
+  return (bad_d || bad_s) ? 1 : 0;
+}

@@ -1,0 +1,203 @@
+"""GPU parity tests: libat2v.so (HIP, gfx950) through its C ABI vs the golden fixtures and the oracle.
+
+Bar: bit-exact verdicts (integer/byte work). Sizes the oracle checks in seconds are compared record by
+record; the full BASELINE sizes (1M) are checked through size-independent properties (every generated
+record valid; exactly the mutated records rejected; verdict bits past n zero; shard/tail invariance).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io
+
+pytestmark = pytest.mark.gpu
+
+CFG_SEED = 0x4154325F
+
+
+@pytest.fixture(scope="module")
+def at2v_mod():
+    import at2v
+    return at2v
+
+
+@pytest.fixture(scope="module")
+def verifier(at2v_mod):
+    v = at2v_mod.BatchVerifier(policy="dalek")
+    yield v
+    v.close()
+
+
+@pytest.fixture(scope="module")
+def verifier_sodium(at2v_mod):
+    v = at2v_mod.BatchVerifier(policy="libsodium")
+    yield v
+    v.close()
+
+
+def _mismatch(got, want, cls=None):
+    bad = np.nonzero(got != want)[0]
+    return f"{bad.size} mismatches at {bad[:10]}" + (f" classes {cls[bad[:10]]}" if cls is not None else "")
+
+
+@pytest.mark.parametrize("name", golden_io.SETS)
+def test_golden_dalek(verifier, golden, name):
+    g = golden[name]
+    got = verifier.verify_batch(g.pk, g.sig, g.msg, g.off)
+    assert np.array_equal(got, g.dalek), _mismatch(got, g.dalek, g.cls)
+
+
+@pytest.mark.parametrize("name", golden_io.SETS)
+def test_golden_libsodium_policy(verifier_sodium, golden, name):
+    g = golden[name]
+    got = verifier_sodium.verify_batch(g.pk, g.sig, g.msg, g.off)
+    assert np.array_equal(got, g.sodium), _mismatch(got, g.sodium, g.cls)
+
+
+def test_info(verifier):
+    info = verifier.info()
+    assert info["cus"] >= 1 and info["grid_blocks"] >= info["cus"] and info["block_threads"] == 256
+
+
+@pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 63, 64, 65, 127, 1000])
+def test_tail_sizes_and_pad_bits(verifier, golden, n):
+    """n not a multiple of 64/32: tail lanes are masked and pad bits are zero."""
+    g = golden["adversarial"]
+    off = g.off[: n + 1]
+    got = verifier.verify_batch(g.pk[:n], g.sig[:n], g.msg, off)
+    assert np.array_equal(got, g.dalek[:n])
+    import ctypes
+    lib = verifier._lib
+    words = np.full((n + 31) // 32 + 1, 0xFFFFFFFF, np.uint32)
+    rc = lib.at2v_verify_batch(verifier._h, g.pk[:n].ctypes.data, g.sig[:n].ctypes.data, g.msg.ctypes.data,
+                               np.ascontiguousarray(off).ctypes.data, n, words.ctypes.data)
+    assert rc == 0
+    if n % 32:
+        assert words[(n - 1) // 32] >> (n % 32) == 0
+    assert words[-1] == 0xFFFFFFFF  # nothing written past ceil(n/32) words
+
+
+def test_empty_batch(verifier):
+    got = verifier.verify_batch(np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8), np.zeros(0, np.uint8),
+                                np.zeros(1, np.uint32))
+    assert got.size == 0
+
+
+def test_unaligned_message_offsets(verifier, golden):
+    """messages starting at arbitrary byte offsets (msg_off[0] > 0, odd lengths)"""
+    g = golden["ragged"]
+    pad = np.zeros(3, np.uint8)
+    msg = np.concatenate([pad, g.msg])
+    got = verifier.verify_batch(g.pk, g.sig, msg, g.off + 3)
+    assert np.array_equal(got, g.dalek)
+
+
+def test_oracle_adversarial_larger(verifier, oracle):
+    """fresh adversarial mix (not the committed fixture) against the oracle, record by record"""
+    pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 1, 100_000, 16384, 100)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    got = verifier.verify_batch(pk, sig, msg, off)
+    assert np.array_equal(got, want), _mismatch(got, want, cls)
+    assert want.sum() > 0.85 * len(want)
+
+
+def test_verify_one_and_drop_mirror(at2v_mod, golden):
+    g = golden["rfc8032"]
+    for i in range(g.n):
+        assert at2v_mod.verify_one(bytes(g.pk[i]), bytes(g.sig[i]), g.message(i))
+        at2v_mod.Signature(bytes(g.sig[i])).verify(g.message(i), at2v_mod.PublicKey(bytes(g.pk[i])))
+    bad = bytearray(g.sig[0])
+    bad[63] ^= 0x80
+    assert not at2v_mod.verify_one(bytes(g.pk[0]), bytes(bad), g.message(0))
+    with pytest.raises(at2v_mod.VerifyError):
+        at2v_mod.Signature(bytes(bad)).verify(g.message(0), at2v_mod.PublicKey(bytes(g.pk[0])))
+
+
+def test_gpu_generator_matches_oracle(verifier, oracle):
+    """GPU keygen+sign of the deterministic generator is bit-exact with the oracle signer"""
+    import torch
+    n, L = 4096, 100
+    d_pk = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    d_msg = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    verifier.gen_records_device(CFG_SEED, 12345, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                d_off.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    pk, sig, msg, off = oracle.gen_records(CFG_SEED, 12345, n, L)
+    assert np.array_equal(d_pk.cpu().numpy().reshape(n, 32), pk)
+    assert np.array_equal(d_msg.cpu().numpy(), msg)
+    assert np.array_equal(d_off.cpu().numpy().astype(np.uint32), off)
+    assert np.array_equal(d_sig.cpu().numpy().reshape(n, 64), sig)
+
+
+def test_sign_batch_matches_oracle(verifier, oracle):
+    rng = np.random.default_rng(5)
+    n = 300
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    lens = rng.integers(0, 300, n)
+    msgs = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in lens]
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum(lens)
+    msg = np.frombuffer(b"".join(msgs), np.uint8)
+    pk, sig = verifier.sign_batch(seeds, msg, off)
+    for i in range(0, n, 7):
+        assert bytes(pk[i]) == oracle.public_key(bytes(seeds[i]))
+        assert bytes(sig[i]) == oracle.sign(bytes(seeds[i]), msgs[i])
+    assert verifier.verify_batch(pk, sig, msg, off).all()
+
+
+def test_device_api_full_size_properties(verifier):
+    """BASELINE config 2 size (1M records, 100-byte messages) on device buffers:
+    all valid; flipping one bit in k chosen records rejects exactly those records."""
+    import torch
+    n, L = 1 << 20, 100
+    s = torch.cuda.current_stream().cuda_stream
+    d_pk = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    d_msg = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    d_ver = torch.zeros((n + 31) // 32, dtype=torch.int32, device="cuda")
+    verifier.gen_records_device(CFG_SEED, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                d_off.data_ptr(), s)
+    verifier.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                                 d_ver.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert (d_ver == -1).all().item(), "every generated record must verify"
+    rng = np.random.default_rng(9)
+    idx = np.unique(rng.integers(0, n, 2000))
+    which = rng.integers(0, 3, idx.size)
+    for k, (i, w) in enumerate(zip(idx.tolist(), which.tolist())):
+        bit = int(rng.integers(0, 8))
+        if w == 0:
+            d_sig[i * 64 + int(rng.integers(0, 64))] ^= (1 << bit)
+        elif w == 1:
+            d_msg[i * L + int(rng.integers(0, L))] ^= (1 << bit)
+        else:
+            d_pk[i * 32 + int(rng.integers(0, 32))] ^= (1 << bit)
+    verifier.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                                 d_ver.data_ptr(), s)
+    torch.cuda.synchronize()
+    import at2v
+    ok = at2v.unpack_verdicts(d_ver.cpu().numpy().view(np.uint32), n)
+    rejected = np.nonzero(~ok)[0]
+    assert np.array_equal(rejected, idx), f"{rejected.size} rejected vs {idx.size} mutated"
+
+
+def test_repeat_determinism(verifier, golden):
+    g = golden["adversarial"]
+    a = verifier.verify_batch(g.pk, g.sig, g.msg, g.off)
+    b = verifier.verify_batch(g.pk, g.sig, g.msg, g.off)
+    assert np.array_equal(a, b)
+
+
+def test_multi_gpu_context_if_available(at2v_mod, golden):
+    import torch
+    ng = torch.cuda.device_count()
+    if ng < 2:
+        pytest.skip("single GPU box")
+    v = at2v_mod.BatchVerifier(num_gpus=ng)
+    g = golden["adversarial"]
+    assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek)
+    v.close()
