@@ -26,6 +26,26 @@
 #define AT2V_BIAS26 (1 << 25)
 #define AT2V_BIAS25 (1 << 24)
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// 2*x as a full-rate v_add_u32 (LLVM would emit the half-rate v_lshlrev_b32 on gfx950)
+__device__ AT2V_INLINE int32_t at2v_dbl32(int32_t x) {
+  int32_t r;
+  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+#define AT2V_X2(x) at2v_dbl32(x)
+#ifndef AT2V_FE_ASM_BLOCKS
+// Column MADs as asm blocks (tools/gen_fe.py emit_block_asm): one v_mad_i64_i32 per column per block,
+// the rounding bias as the SGPR addend of the first block. Plain C lets LLVM re-associate the bias
+// out of the chains (10 extra 64-bit adds per multiply).
+#define AT2V_FE_ASM_BLOCKS 1
+#endif
+#else
+#define AT2V_X2(x) (2 * (x))
+#undef AT2V_FE_ASM_BLOCKS
+#define AT2V_FE_ASM_BLOCKS 0
+#endif
+
 namespace at2v {
 
 struct fe {
@@ -60,25 +80,31 @@ AT2V_HD AT2V_INLINE void fe_select(fe& h, const fe& f, const fe& g, int b) {
 
 // Balanced floor-carry of the 10 biased column accumulators of a product (each column was
 // initialised with its rounding bias 2^(w-1)): r_i = (h_i mod 2^w) - 2^(w-1), carry = h_i >> w.
-// The carry out of limb 9 has weight 2^255 = 19 (mod p) and is folded into limb 0, which is
-// carried once more into limb 1.
+// Two interleaved chains (critical path 7 carries instead of 11):
+//   A: 0 -> 1 -> 2 -> 3 -> 4' -> 5          B: 4 -> 5 -> 6 -> 7 -> 8 -> 9 -> (x19) 0' -> 1
+// Limb 4 is carried twice (its second pass re-adds the bias); limbs 1 and 5 end with a small spill
+// (< 2^16), accounted for in tools/gen_fe.py carried_bound().
+#define AT2V_EXT26(h) (((int32_t)(h) & 0x3ffffff) - (1 << 25))
+#define AT2V_EXT25(h) (((int32_t)(h) & 0x1ffffff) - (1 << 24))
 AT2V_HD AT2V_INLINE void fe_carry_wide(fe& r, int64_t h0, int64_t h1, int64_t h2, int64_t h3, int64_t h4, int64_t h5,
                                        int64_t h6, int64_t h7, int64_t h8, int64_t h9) {
-  int64_t c;
-  c = h0 >> 26; h1 += c; r.v[0] = ((int32_t)h0 & 0x3ffffff) - (1 << 25);
-  c = h1 >> 25; h2 += c; r.v[1] = ((int32_t)h1 & 0x1ffffff) - (1 << 24);
-  c = h2 >> 26; h3 += c; r.v[2] = ((int32_t)h2 & 0x3ffffff) - (1 << 25);
-  c = h3 >> 25; h4 += c; r.v[3] = ((int32_t)h3 & 0x1ffffff) - (1 << 24);
-  c = h4 >> 26; h5 += c; r.v[4] = ((int32_t)h4 & 0x3ffffff) - (1 << 25);
-  c = h5 >> 25; h6 += c; r.v[5] = ((int32_t)h5 & 0x1ffffff) - (1 << 24);
-  c = h6 >> 26; h7 += c; r.v[6] = ((int32_t)h6 & 0x3ffffff) - (1 << 25);
-  c = h7 >> 25; h8 += c; r.v[7] = ((int32_t)h7 & 0x1ffffff) - (1 << 24);
-  c = h8 >> 26; h9 += c; r.v[8] = ((int32_t)h8 & 0x3ffffff) - (1 << 25);
-  c = h9 >> 25;          r.v[9] = ((int32_t)h9 & 0x1ffffff) - (1 << 24);
-  int64_t t0 = (int64_t)r.v[0] + c * 19 + (1 << 25);
-  c = t0 >> 26;
-  r.v[0] = ((int32_t)t0 & 0x3ffffff) - (1 << 25);
-  r.v[1] += (int32_t)c;
+  int64_t ca, cb;
+  ca = h0 >> 26; h1 += ca; r.v[0] = AT2V_EXT26(h0);
+  cb = h4 >> 26; h5 += cb; const int32_t t4 = AT2V_EXT26(h4);
+  ca = h1 >> 25; h2 += ca; r.v[1] = AT2V_EXT25(h1);
+  cb = h5 >> 25; h6 += cb; const int32_t t5 = AT2V_EXT25(h5);
+  ca = h2 >> 26; h3 += ca; r.v[2] = AT2V_EXT26(h2);
+  cb = h6 >> 26; h7 += cb; r.v[6] = AT2V_EXT26(h6);
+  ca = h3 >> 25; r.v[3] = AT2V_EXT25(h3);
+  const int64_t h4b = (int64_t)t4 + ca + (1 << 25);
+  cb = h7 >> 25; h8 += cb; r.v[7] = AT2V_EXT25(h7);
+  ca = h4b >> 26; r.v[5] = t5 + (int32_t)ca; r.v[4] = AT2V_EXT26(h4b);
+  cb = h8 >> 26; h9 += cb; r.v[8] = AT2V_EXT26(h8);
+  cb = h9 >> 25; r.v[9] = AT2V_EXT25(h9);
+  const int64_t h0b = (int64_t)r.v[0] + cb * 19 + (1 << 25);
+  cb = h0b >> 26;
+  r.v[0] = AT2V_EXT26(h0b);
+  r.v[1] += (int32_t)cb;
 }
 
 // Balanced carry of an element with int32 limbs (any |v_i| < 2^30): result is "carried".

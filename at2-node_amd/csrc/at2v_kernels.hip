@@ -15,6 +15,10 @@
 
 namespace at2v {
 
+#ifndef AT2V_VERIFY_WAVES_PER_SIMD
+#define AT2V_VERIFY_WAVES_PER_SIMD 2  // register budget: 512 / waves VGPR+AGPR per lane
+#endif
+
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kTabAGranules = 9 * 10;  // 9 entries x 10 x 16 B
@@ -85,7 +89,7 @@ __device__ AT2V_INLINE uint32_t load_u32_guarded(const uint8_t* buf, uint32_t a,
   return v;
 }
 
-__global__ __launch_bounds__(kBlock) void verify_kernel(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
                                                         const uint8_t* __restrict__ msg, uint32_t msg_total,
                                                         const uint32_t* __restrict__ off, uint32_t n, int policy,
                                                         uint32_t* __restrict__ verdicts, int4* __restrict__ scratch) {
@@ -116,7 +120,8 @@ __global__ __launch_bounds__(kBlock) void verify_kernel(const uint8_t* __restric
       const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
       return __builtin_amdgcn_alignbit(hi, lo, sh);
     };
-    int ok = verify_core(Rw, Aw, Sw, len, msgword, policy, ta, tb);
+    const uint8_t* rp = sig + (size_t)ii * 64;
+    int ok = verify_core(Rw, Aw, Sw, len, msgword, policy, ta, tb, [&](uint32_t r[8]) { load8(r, rp); });
     ok &= live;
     const uint64_t mask = __ballot(ok);
     if (lane == 0) {

@@ -88,8 +88,9 @@ AT2V_HD AT2V_INLINE void sha512_prefixed(uint64_t h[8], const uint32_t* prefix, 
       for (int half = 0; half < 2; ++half) {
         const uint32_t pos = (b << 7) + 8 * t + 4 * half;  // stream byte position (4-aligned)
         uint32_t le;
-        if (pos < (uint32_t)(4 * NPW)) {
-          le = prefix[pos >> 2];
+        // the prefix (<= 64 bytes) lives in block 0 only: static register index, no scratch
+        if (2 * t + half < NPW && b == 0) {
+          le = prefix[(2 * t + half) < NPW ? (2 * t + half) : 0];
         } else {
           const uint32_t mo = pos - 4 * NPW;                 // message byte offset
           uint32_t v = 0;

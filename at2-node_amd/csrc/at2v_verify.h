@@ -52,9 +52,9 @@ AT2V_HD AT2V_INLINE int enc_small_order(const uint32_t s[8]) {
 // Table access policies.
 //   TabA: void store(int e, const ge_cached&); void load(int e, ge_cached&)   (per lane, e in 0..8)
 //   TabB: void load(int e, ge_niels&)                                          (shared, e in 0..128)
-template <class TabA, class TabB, class MsgWord>
+template <class TabA, class TabB, class MsgWord, class RLoad>
 AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
-                                    MsgWord msgword, int policy, TabA& ta, const TabB& tb) {
+                                    MsgWord msgword, int policy, TabA& ta, const TabB& tb, RLoad rload) {
   // V1: s < l
   int ok = sc_is_canonical(Sw);
   if (policy == POLICY_LIBSODIUM_1_0_18) {
@@ -117,13 +117,13 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
     ge_p1p1_to_p2(R2, t);
   }
   for (int i = 62; i >= 0; --i) {
-    const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
-    ta.load(d < 0 ? -d : d, ca);  // issued before the doublings: latency hidden behind them
     for (int r = 0; r < 3; ++r) {
       ge_p2_dbl(t, R2);
       ge_p1p1_to_p2(R2, t);
     }
     ge_p2_dbl(t, R2);
+    const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
+    ta.load(d < 0 ? -d : d, ca);
     ge_p1p1_to_p3(R3, t);
     ge_cached_cneg(ca, d < 0);
     ge_add(t, R3, ca);
@@ -137,11 +137,12 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
     ge_p1p1_to_p2(R2, t);
   }
   // V5/V6: canonical encoding of R' == R bytes
-  uint32_t enc[8];
+  uint32_t enc[8], Rr[8];
   ge_p2_tobytes(enc, R2);
+  rload(Rr);  // R re-read at the end rather than kept live across the ladder
   int eq = 1;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) eq &= enc[i] == Rw[i];
+  for (int i = 0; i < 8; ++i) eq &= enc[i] == Rr[i];
   return ok & eq;
 }
 

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""A/B kernel-time comparison of libat2v builds, interleaved rounds in ONE process (guide rule 24).
+usage: python3 tools/ab_bench.py lib1.so lib2.so ... [--n 1048576] [--rounds 5]
+Also checks every build returns all-valid verdicts for the generated batch."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "at2-node_amd"))
+import at2v  # noqa: E402
+
+
+def open_lib(path):
+    lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+    P = ctypes.c_void_p
+    lib.at2v_create.argtypes = [P, ctypes.POINTER(P)]
+    lib.at2v_verify_batch_device.argtypes = [P, P, P, P, ctypes.c_size_t, P, ctypes.c_size_t, P, P]
+    lib.at2v_gen_records_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
+                                            P, P, P, P, P]
+    h = P()
+    assert lib.at2v_create(None, ctypes.byref(h)) == 0
+    return lib, h
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--msg-len", type=int, default=100)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    n, L = a.n, a.msg_len
+    libs = [open_lib(p) for p in a.libs]
+    s = torch.cuda.current_stream()
+    d_pk = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_sig = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_msg = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+    d_ver = torch.zeros((n + 31) // 32, dtype=torch.int32, device="cuda")
+    lib0, h0 = libs[0]
+    assert lib0.at2v_gen_records_device(h0, 0x4154325F, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                        d_off.data_ptr(), s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    times = {p: [] for p in a.libs}
+    for r in range(a.rounds + 1):
+        for p, (lib, h) in zip(a.libs, libs):
+            d_ver.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            assert lib.at2v_verify_batch_device(h, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L,
+                                                d_off.data_ptr(), n, d_ver.data_ptr(), s.cuda_stream) == 0
+            e1.record(s)
+            torch.cuda.synchronize()
+            ok = bool((d_ver == -1).all().item())
+            if r > 0:
+                times[p].append(e0.elapsed_time(e1))
+            assert ok, f"{p}: wrong verdicts"
+    for p in a.libs:
+        t = np.array(times[p])
+        print(f"{os.path.basename(p):28s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  -> {n / np.median(t) / 1e3:8.2f} M verifies/s")
+
+
+if __name__ == "__main__":
+    main()

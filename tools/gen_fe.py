@@ -89,8 +89,8 @@ MAX64 = 2**63 - 1
 
 
 def carried_bound(i):
-    # balanced limb after carry chain (+ spill on limb 1 from the final 0->1 carry)
-    return (1 << (W[i] - 1)) + (1 << 16 if i == 1 else 0) + (19 if i == 0 else 0)
+    # balanced limb after carry chain (+ spill on limbs 1 and 5 from the second carries into them)
+    return (1 << (W[i] - 1)) + (1 << 16 if i in (1, 5) else 0) + (19 if i == 0 else 0)
 
 
 def input_bound(i, terms=3):
@@ -184,6 +184,44 @@ def check_cols(cols, name):
     return worst
 
 
+def emit_block_asm(cols):
+    """device variant: all MADs of one multiply/square in ONE asm statement, column-interleaved
+    (step t issues the t-th MAD of every column, so dependent MADs are <= 10 instructions apart),
+    with the rounding bias as the SGPR addend of step 0. One hazard pad per field op instead of one
+    per MAD; LLVM cannot re-associate the bias out of the chains. Returns C++ lines defining h0..h9."""
+    out = []
+    nsteps = max(len(c) for c in cols)
+    out.append("  int64_t h0, h1, h2, h3, h4, h5, h6, h7, h8, h9;")
+    ins = []
+    idx = {}
+
+    def opnd(expr, cons):
+        key = (expr, cons)
+        if key not in idx:
+            idx[key] = len(ins)
+            ins.append(key)
+        return idx[key]
+    lines = []
+    for t in range(nsteps):
+        for k in range(10):
+            if len(cols[k]) <= t:
+                continue
+            fa, gb = cols[k][len(cols[k]) - 1 - t][0], cols[k][len(cols[k]) - 1 - t][1]
+            ia, ib = opnd(fa, "v"), opnd(gb, "v")
+            if t == 0:
+                ic = opnd(f"(int64_t)AT2V_BIAS{W[k]}", "s")
+                lines.append(f"v_mad_i64_i32 %{k}, vcc, %{10 + ia}, %{10 + ib}, %{10 + ic}")
+            else:
+                lines.append(f"v_mad_i64_i32 %{k}, vcc, %{10 + ia}, %{10 + ib}, %{k}")
+    outs = ", ".join(f'"=&v"(h{k})' for k in range(10))
+    inl = ", ".join(f'"{c}"({e})' for e, c in ins)
+    out.append('  asm("' + "\\n\\t".join(lines) + '"')
+    out.append('      : ' + outs)
+    out.append('      : ' + inl)
+    out.append('      : "vcc");')
+    return out
+
+
 def emit_fn(name, cols, need, sig, src_g):
     out = []
     out.append(f"AT2V_HD AT2V_INLINE void {name}{sig} {{")
@@ -193,13 +231,21 @@ def emit_fn(name, cols, need, sig, src_g):
     for (op, idx, s) in sorted(need):
         if s == 1:
             continue
-        out.append(f"  const int32_t {op}{idx}_{s} = {s} * {op}{idx};")
+        if s == 2:
+            out.append(f"  const int32_t {op}{idx}_2 = AT2V_X2({op}{idx});")
+        elif s == 4 and (op, idx, 2) in need:
+            out.append(f"  const int32_t {op}{idx}_4 = AT2V_X2({op}{idx}_2);")
+        else:
+            out.append(f"  const int32_t {op}{idx}_{s} = {s} * {op}{idx};")
+    out.append("#if AT2V_FE_ASM_BLOCKS")
+    out += emit_block_asm(cols)
+    out.append("#else")
     for k in range(10):
-        acc = f"(int64_t)AT2V_BIAS{W[k]}"
-        expr = acc
+        expr = f"(int64_t)AT2V_BIAS{W[k]}"
         for fa, gb, *_ in cols[k]:
             expr = f"AT2V_MAD({fa}, {gb}, {expr})"
         out.append(f"  int64_t h{k} = {expr};")
+    out.append("#endif")
     out.append("  fe_carry_wide(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);")
     out.append("}")
     return "\n".join(out)

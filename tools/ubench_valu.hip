@@ -83,6 +83,22 @@ __global__ __launch_bounds__(256) void kern(uint32_t* out, uint32_t a0, uint32_t
     if constexpr (OP == 24) { BODY32("v_and_b32 %0, %1, %0") }
     if constexpr (OP == 25) { BODY32("v_mul_f32 %0, %1, %0") }
     if constexpr (OP == 26) { BODY32("v_sub_u32 %0, %1, %0") }
+    if constexpr (OP == 27) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) { uint64_t cy; asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(q[c]), "=s"(cy) : "v"(a), "v"(b)); }
+    }
+    if constexpr (OP == 28) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) asm volatile("v_ashrrev_i64 %0, 7, %0" : "+v"(q[c]));
+    }
+    if constexpr (OP == 29) {  // dependent mad chain, 1 chain per lane (latency)
+      uint64_t cy; asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(q[0]), "=s"(cy) : "v"(a), "v"(b));
+    }
+    if constexpr (OP == 30) { BODY32("v_cndmask_b32 %0, %1, %0, vcc") }
+    if constexpr (OP == 31) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) asm volatile("v_mov_b64 %0, %1" : "=v"(q[c]) : "v"(q[(c + 1) % CH]));
+    }
   }
   uint32_t acc = 0;
 #pragma unroll
@@ -94,7 +110,7 @@ static const char* NAMES[] = {"v_add_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mu
                               "v_mad_u32_u24", "v_mad_u64_u32(+carry)", "v_fma_f64", "v_dot2_u32_u16", "v_lshl_add_u64",
                               "v_add3_u32", "v_alignbit_b32", "v_add_co+v_addc_co (2 instr)", "v_lshrrev_b64",
                               "v_bfe_u32", "u64 a*b+q (compiler)", "v_mad_u32_u16", "v_lshl_add_u32", "v_xor_b32", "v_add_u32_e64", "v_fma_f32", "v_pk_fma_f32",
-                              "v_add_co_u32", "v_lshlrev_b32", "v_and_b32", "v_mul_f32", "v_sub_u32"};
+                              "v_add_co_u32", "v_lshlrev_b32", "v_and_b32", "v_mul_f32", "v_sub_u32", "v_mad_i64_i32", "v_ashrrev_i64", "mad_i64 dependent (1 chain)", "v_cndmask_b32", "v_mov_b64"};
 
 template <int OP>
 int run(uint32_t* dout, int blocks) {
@@ -113,7 +129,7 @@ int run(uint32_t* dout, int blocks) {
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     if (ms < best) best = ms;
   }
-  double n = (double)blocks * 256 * ITERS * CH * (OP == 12 ? 2 : 1);
+  double n = (double)blocks * 256 * ITERS * (OP == 29 ? 1 : CH) * (OP == 12 ? 2 : 1);
   double rate = n / (best * 1e-3);
   // full rate reference: 256 CU x 128 lanes/clk x 2.4 GHz
   printf("%-30s %8.3f ms  %8.2f Tlane-op/s  (%.3f of 7.86e13 full-rate)\n", NAMES[OP], best, rate / 1e12,
@@ -135,6 +151,9 @@ int main() {
   run<16>(dout, blocks); run<17>(dout, blocks); run<18>(dout, blocks); run<19>(dout, blocks);
   run<20>(dout, blocks); run<21>(dout, blocks); run<22>(dout, blocks); run<23>(dout, blocks);
   run<24>(dout, blocks); run<25>(dout, blocks); run<26>(dout, blocks);
+  run<27>(dout, blocks); run<28>(dout, blocks); run<30>(dout, blocks); run<31>(dout, blocks);
+  printf("-- 1 wave/SIMD, 1 dependent chain --\n");
+  run<29>(dout, blocks/8);
   printf("-- at 4 waves/SIMD --\n");
   run<0>(dout, blocks/2); run<6>(dout, blocks/2); run<10>(dout, blocks/2); run<20>(dout, blocks/2);
   printf("-- at 1 wave/SIMD --\n");
