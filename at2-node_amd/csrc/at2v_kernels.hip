@@ -24,20 +24,46 @@ constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kTabAGranules = 9 * 10;  // 9 entries x 10 x 16 B
 constexpr size_t kScratchPerWave = (size_t)kTabAGranules * 64 * 16;
 
+// Per-lane table [0..8](-A) in global scratch. Layout: lane-contiguous, 9 entries x 160 B per lane
+// (1440 B), so the 10 16-byte loads of one entry hit the same 2 cache lines per lane (L1-resident
+// across the 10 loads) whatever entry index each lane selects. (r01 interleaved lanes per 16-byte
+// granule: lanes with different digits then touched up to 9 different 1 KiB rows per load,
+// ~9x read amplification — profiles/r01 FETCH_SIZE.)
 struct DevTabA {
-  int4* base;  // this wave's slice
+  int4* base;   // this lane's 1440-byte slot (global)
+  int4* stage;  // this wave's 10 x 1 KiB LDS staging buffer for the prefetched entry
   int lane;
   __device__ AT2V_INLINE void store(int e, const ge_cached& c) const {
     const int32_t* w = reinterpret_cast<const int32_t*>(&c);
 #pragma unroll
-    for (int q = 0; q < 10; ++q)
-      base[(e * 10 + q) * 64 + lane] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (int q = 0; q < 10; ++q) base[e * 10 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
   __device__ AT2V_INLINE void load(int e, ge_cached& c) const {
     int32_t* w = reinterpret_cast<int32_t*>(&c);
 #pragma unroll
     for (int q = 0; q < 10; ++q) {
-      const int4 v = base[(e * 10 + q) * 64 + lane];
+      const int4 v = base[e * 10 + q];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+  }
+  // LDS-DMA (global_load_lds_dwordx4): entry e of every lane -> stage[q][lane], no VGPRs held while the
+  // window's four doublings run
+  __device__ AT2V_INLINE void prefetch(int e) const {
+#pragma unroll
+    for (int q = 0; q < 10; ++q)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + e * 10 + q),
+                                       (__attribute__((address_space(3))) void*)(stage + q * 64), 16,
+                                       0, 0);
+  }
+  __device__ AT2V_INLINE void load_prefetched(ge_cached& c) const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t* w = reinterpret_cast<int32_t*>(&c);
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const int4 v = stage[q * 64 + lane];
       w[4 * q] = v.x;
       w[4 * q + 1] = v.y;
       w[4 * q + 2] = v.z;
@@ -94,13 +120,14 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
                                                         const uint32_t* __restrict__ off, uint32_t n, int policy,
                                                         uint32_t* __restrict__ verdicts, int4* __restrict__ scratch) {
   __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   stage_btab(btab);
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t nwords = (n + 31) / 32;
-  DevTabA ta{scratch + (size_t)wave * (kTabAGranules * 64), lane};
+  DevTabA ta{scratch + ((size_t)wave * 64 + lane) * kTabAGranules, astage + (threadIdx.x >> 6) * 640, lane};
   LdsTabB tb{btab};
   for (uint32_t chunk = wave; chunk < nchunks; chunk += nwaves) {
     const uint32_t i = chunk * 64 + lane;

@@ -50,7 +50,8 @@ AT2V_HD AT2V_INLINE int enc_small_order(const uint32_t s[8]) {
 }
 
 // Table access policies.
-//   TabA: void store(int e, const ge_cached&); void load(int e, ge_cached&)   (per lane, e in 0..8)
+//   TabA: void store(int e, const ge_cached&); void load(int e, ge_cached&);  (per lane, e in 0..8)
+//         void prefetch(int e); void load_prefetched(ge_cached&)   (asynchronous load of one entry)
 //   TabB: void load(int e, ge_niels&)                                          (shared, e in 0..128)
 template <class TabA, class TabB, class MsgWord, class RLoad>
 AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
@@ -117,13 +118,14 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
     ge_p1p1_to_p2(R2, t);
   }
   for (int i = 62; i >= 0; --i) {
+    const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
+    ta.prefetch(d < 0 ? -d : d);  // lands while the four doublings run
     for (int r = 0; r < 3; ++r) {
       ge_p2_dbl(t, R2);
       ge_p1p1_to_p2(R2, t);
     }
     ge_p2_dbl(t, R2);
-    const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
-    ta.load(d < 0 ? -d : d, ca);
+    ta.load_prefetched(ca);
     ge_p1p1_to_p3(R3, t);
     ge_cached_cneg(ca, d < 0);
     ge_add(t, R3, ca);

@@ -20,11 +20,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
 
 CFG_SEED = 0x4154325F
-# nominal algorithmic work per verify, 32-bit VALU lane-ops (10-limb schoolbook estimate)
-ALG_OPS_PER_VERIFY = 1.1e6
-# int32 VALU issue peak per GPU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md chip table);
-# v_mad_i64_i32 (the field-multiply instruction) issues at half this rate (profiles/r01_ubench_valu.txt)
-VALU_PEAK_OPS = 256 * 128 * 2.4e9
+# Algorithmic work per verify: the verify path performs 1589 field multiplications and
+# 1517 field squarings (decompress 255S+21M, table 64M, ladder 1008S+1491M, inversion+encode 254S+13M);
+# a 10-limb radix-2^25.5 multiplication is 100 and a squaring 55 32x32->64 multiply-accumulates.
+FIELD_MUL_PER_VERIFY = 1589
+FIELD_SQ_PER_VERIFY = 1517
+MAC_PER_VERIFY = 100 * FIELD_MUL_PER_VERIFY + 55 * FIELD_SQ_PER_VERIFY  # 242,335
+# Peak: v_mad_i64_i32 issues at half the VALU rate on gfx950 (profiles/r01_ubench_valu.txt): one wave64
+# instruction per 4 cycles per SIMD = 16 lane-MACs/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz.
+MAC_PEAK = 256 * 4 * 16 * 2.4e9  # 3.93e13 MAC/s
 HBM_PEAK_GBS = 8000.0
 
 
@@ -36,7 +40,7 @@ def parse():
     ap.add_argument("--records-per-gpu", type=int, default=1 << 20)
     ap.add_argument("--msg-len", type=int, default=100)
     ap.add_argument("--policy", default="dalek")
-    ap.add_argument("--cpu-sample", type=int, default=32768, help="records for the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=262144, help="records for the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     return ap.parse_args()
 
@@ -48,6 +52,7 @@ def main():
     import torch.distributed as dist
 
     import at2v
+    from at2v import dist as at2dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -81,7 +86,7 @@ def main():
         v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
                               d_ver.data_ptr(), s)
         if world > 1:
-            dist.all_gather_into_tensor(d_all, d_ver)
+            at2dist.gather_verdicts(d_ver, world)
 
     for _ in range(args.warmup):
         step()
@@ -100,7 +105,7 @@ def main():
                               d_ver.data_ptr(), s)
         kev[k][1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(d_all, d_ver)
+            d_all = at2dist.gather_verdicts(d_ver, world)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -124,7 +129,7 @@ def main():
     total = n * world * args.steps
     value = total / elapsed
     per_gpu_kernel_rate = n / (kernel_ms * 1e-3)
-    achieved = per_gpu_kernel_rate * ALG_OPS_PER_VERIFY / 1e12
+    achieved = per_gpu_kernel_rate * MAC_PER_VERIFY / 1e12
     info = v.info()
 
     out = None
@@ -157,12 +162,13 @@ def main():
             "roofline": {
                 "bound": "valu",
                 "achieved": achieved,
-                "peak": VALU_PEAK_OPS / 1e12,
-                "unit": "Tops/s (int32 lane-ops)",
-                "frac": achieved * 1e12 / VALU_PEAK_OPS,
+                "peak": MAC_PEAK / 1e12,
+                "unit": "Tops/s (32x32->64 integer MAC, v_mad_i64_i32)",
+                "frac": achieved * 1e12 / MAC_PEAK,
                 "traffic": None,
-                "alg_ops_per_verify": ALG_OPS_PER_VERIFY,
+                "alg_macs_per_verify": MAC_PER_VERIFY,
                 "alg_bytes_per_verify": 32 + 64 + L + 4,
+                "hbm_gbs": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9,
                 "hbm_frac": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9 / HBM_PEAK_GBS,
             },
         }

@@ -12,8 +12,11 @@ using namespace at2v;
 
 struct HostTabA {
   ge_cached e[9];
+  int pending = 0;
   void store(int i, const ge_cached& c) { e[i] = c; }
   void load(int i, ge_cached& c) const { c = e[i]; }
+  void prefetch(int i) { pending = i; }
+  void load_prefetched(ge_cached& c) const { c = e[pending]; }
 };
 struct HostTabB {
   void load(int i, ge_niels& n) const {
