@@ -138,6 +138,20 @@ AT2V_HD AT2V_INLINE void ge_niels_cneg(ge_niels& r, int neg) {
   }
 }
 
+// affine Niels form (y+x, y-x, 2dxy) of a p2 point (one inversion), carried limbs
+AT2V_HD AT2V_INLINE void ge_p2_to_niels(ge_niels& r, const ge_p2& p) {
+  fe zi, x, y;
+  fe_invert(zi, p.Z);
+  fe_mul(x, p.X, zi);
+  fe_mul(y, p.Y, zi);
+  fe_add(r.ypx, y, x);
+  fe_carry32(r.ypx);
+  fe_sub(r.ymx, y, x);
+  fe_carry32(r.ymx);
+  fe_mul(r.xy2d, x, y);
+  fe_mul(r.xy2d, r.xy2d, FE_D2);
+}
+
 // enc(P) = canonical y with bit 255 = x & 1 (x = X/Z, y = Y/Z), as 8 LE words
 AT2V_HD AT2V_INLINE void ge_p2_tobytes(uint32_t out[8], const ge_p2& p) {
   fe zi, x, y;

@@ -22,7 +22,9 @@ namespace at2v {
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kTabAGranules = 9 * 10;  // 9 entries x 10 x 16 B
-constexpr size_t kScratchPerWave = (size_t)kTabAGranules * 64 * 16;
+constexpr int kParkGranules = 8;       // parked R' (X, Y, Z: 30 words) of the first chunk of a pair
+constexpr int kLaneGranules = kTabAGranules + kParkGranules;
+constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
 
 // Per-lane table [0..8](-A) in global scratch. Layout: lane-contiguous, 9 entries x 160 B per lane
 // (1440 B), so the 10 16-byte loads of one entry hit the same 2 cache lines per lane (L1-resident
@@ -93,6 +95,39 @@ struct LdsTabB {
   }
 };
 
+// Fixed-base table [0..2^15]B (affine Niels, 8 x 16 B per entry, 4.2 MB) in global memory: L2/MALL
+// resident, read through an LDS-DMA prefetch like the A entries.
+constexpr int kBtab16Entries = (1 << 15) + 1;
+struct DevTabB16 {
+  const int4* base;
+  int4* stage;  // this wave's 8 x 1 KiB LDS staging buffer
+  int lane;
+  __device__ AT2V_INLINE void prefetch(int e) const {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + e * 8 + q),
+                                       (__attribute__((address_space(3))) void*)(stage + q * 64), 16, 0, 0);
+  }
+  __device__ AT2V_INLINE void load_prefetched(ge_niels& n) const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t w[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int4 v = stage[q * 64 + lane];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      n.ypx.v[k] = w[k];
+      n.ymx.v[k] = w[10 + k];
+      n.xy2d.v[k] = w[20 + k];
+    }
+  }
+};
+
 __device__ AT2V_INLINE void stage_btab(int4* lds) {
   const int4* src = reinterpret_cast<const int4*>(AT2V_BTAB);
   for (int i = threadIdx.x; i < AT2V_BTAB_ENTRIES * 8; i += blockDim.x) lds[i] = src[i];
@@ -115,78 +150,96 @@ __device__ AT2V_INLINE uint32_t load_u32_guarded(const uint8_t* buf, uint32_t a,
   return v;
 }
 
-__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
-                                                        const uint8_t* __restrict__ msg, uint32_t msg_total,
-                                                        const uint32_t* __restrict__ off, uint32_t n, int policy,
-                                                        uint32_t* __restrict__ verdicts, int4* __restrict__ scratch) {
-  __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab16) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
-  stage_btab(btab);
+  __shared__ int4 bstage[kWavesPerBlock * 8 * 64];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t nwords = (n + 31) / 32;
-  DevTabA ta{scratch + ((size_t)wave * 64 + lane) * kTabAGranules, astage + (threadIdx.x >> 6) * 640, lane};
-  LdsTabB tb{btab};
-  for (uint32_t chunk = wave; chunk < nchunks; chunk += nwaves) {
-    const uint32_t i = chunk * 64 + lane;
-    const bool live = i < n;
-    const uint32_t ii = live ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
-    uint32_t Rw[8], Sw[8], Aw[8];
-    load8(Rw, sig + (size_t)ii * 64);
-    load8(Sw, sig + (size_t)ii * 64 + 32);
-    load8(Aw, pk + (size_t)ii * 32);
-    const uint32_t o0 = off[ii];
-    const uint32_t len = off[ii + 1] - o0;
-    auto msgword = [&](uint32_t j) -> uint32_t {
-      const uint32_t a = o0 + 4 * j;
-      const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
-      const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
-      if (sh == 0) return lo;
-      const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
-      return __builtin_amdgcn_alignbit(hi, lo, sh);
-    };
-    const uint8_t* rp = sig + (size_t)ii * 64;
-    int ok = verify_core(Rw, Aw, Sw, len, msgword, policy, ta, tb, [&](uint32_t r[8]) { load8(r, rp); });
-    ok &= live;
-    const uint64_t mask = __ballot(ok);
-    if (lane == 0) {
-      verdicts[2 * chunk] = (uint32_t)mask;
-      if (2 * chunk + 1 < nwords) verdicts[2 * chunk + 1] = (uint32_t)(mask >> 32);
+  int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
+  DevTabA ta{slot, astage + (threadIdx.x >> 6) * 640, lane};
+  DevTabB16 tb{btab16, bstage + (threadIdx.x >> 6) * 512, lane};
+  int4* park = slot + kTabAGranules;
+  // Chunks are taken in pairs (c, c + nwaves): one field inversion serves both (Montgomery's trick).
+  // The ladder body appears once (rolled loop over the pair); R'_1 is parked in scratch meanwhile.
+  for (uint32_t c = wave; c < nchunks; c += 2 * nwaves) {
+    const uint32_t c2 = c + nwaves;
+    const int npair = c2 < nchunks ? 2 : 1;
+    int ok0 = 0, ok1 = 0;
+    ge_p2 Rp;
+#pragma unroll 1
+    for (int h = 0; h < npair; ++h) {
+      const uint32_t chunk = h ? c2 : c;
+      const uint32_t i = chunk * 64 + lane;
+      const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
+      uint32_t Rw[8], Sw[8], Aw[8];
+      load8(Rw, sig + (size_t)ii * 64);
+      load8(Sw, sig + (size_t)ii * 64 + 32);
+      load8(Aw, pk + (size_t)ii * 32);
+      const uint32_t o0 = off[ii];
+      const uint32_t len = off[ii + 1] - o0;
+      auto msgword = [&](uint32_t j) -> uint32_t {
+        const uint32_t a = o0 + 4 * j;
+        const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+        const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+        if (sh == 0) return lo;
+        const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+        return __builtin_amdgcn_alignbit(hi, lo, sh);
+      };
+      const int ok = verify_ladder(Rp, Rw, Aw, Sw, len, msgword, policy, ta, tb) & (i < n);
+      ok0 = h ? ok0 : ok;
+      ok1 = h ? ok : ok1;
+      if (h == 0 && npair == 2) {  // park R'_1 in this lane's scratch slot while the second chunk runs
+        const int32_t* w = reinterpret_cast<const int32_t*>(&Rp);
+#pragma unroll
+        for (int q = 0; q < 7; ++q) park[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        park[7] = make_int4(w[28], w[29], 0, 0);
+      }
+    }
+    ge_p2 R1;  // first chunk's R'
+    fe zi1, zi2;
+    if (npair == 2) {
+      int32_t* w = reinterpret_cast<int32_t*>(&R1);
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        const int4 v = park[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
+      const int4 v = park[7];
+      w[28] = v.x;
+      w[29] = v.y;
+      fe z12, inv;
+      fe_mul(z12, R1.Z, Rp.Z);
+      fe_invert(inv, z12);
+      fe_mul(zi1, inv, Rp.Z);
+      fe_mul(zi2, inv, R1.Z);
+    } else {
+      R1 = Rp;
+      fe_invert(zi1, Rp.Z);
+    }
+#pragma unroll 1
+    for (int h = 0; h < npair; ++h) {
+      const uint32_t chunk = h ? c2 : c;
+      const uint32_t i = chunk * 64 + lane;
+      const uint32_t ii = i < n ? i : n - 1;
+      uint32_t Rr[8];
+      load8(Rr, sig + (size_t)ii * 64);
+      const int good = (h ? ok1 : ok0) & verify_finish(h ? Rp : R1, h ? zi2 : zi1, Rr);
+      const uint64_t mask = __ballot(good);
+      if (lane == 0) {
+        verdicts[2 * chunk] = (uint32_t)mask;
+        if (2 * chunk + 1 < nwords) verdicts[2 * chunk + 1] = (uint32_t)(mask >> 32);
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------ signing side
-
-// [s]B for a reduced scalar s < l: Horner over 32 signed radix-256 digits, 8 doublings per digit
-template <class TabB>
-__device__ AT2V_INLINE void ge_scalarmult_base(ge_p2& out, const uint32_t s[8], const TabB& tb) {
-  uint32_t sd[8];
-  sc_recode8(sd, s);
-  ge_p3 R3;
-  ge_p1p1 t;
-  ge_niels nb;
-  ge_p3_identity(R3);
-  ge_p2 R2;
-  for (int j = 31; j >= 0; --j) {
-    if (j != 31) {
-      for (int r = 0; r < 7; ++r) {
-        ge_p2_dbl(t, R2);
-        ge_p1p1_to_p2(R2, t);
-      }
-      ge_p2_dbl(t, R2);
-      ge_p1p1_to_p3(R3, t);
-    }
-    const int e = (int)((sd[j >> 2] >> (8 * (j & 3))) & 255) - 128;
-    tb.load(e < 0 ? -e : e, nb);
-    ge_niels_cneg(nb, e < 0);
-    ge_madd(t, R3, nb);
-    ge_p1p1_to_p2(R2, t);
-  }
-  out = R2;
-}
 
 __device__ AT2V_INLINE void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]) {
   uint32_t x[16];
@@ -370,17 +423,48 @@ __global__ __launch_bounds__(kBlock) void sign_kernel(const uint8_t* __restrict_
   for (int q = 0; q < 16; ++q) sgo[q] = sigw[q];
 }
 
+// [j]B, j = 0..2^15, affine Niels, 32 words per entry (30 + 2 pad): built once per context
+__global__ __launch_bounds__(kBlock) void build_btab16_kernel(int4* __restrict__ out) {
+  __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+  stage_btab(btab);
+  LdsTabB tb{btab};
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (uint32_t)kBtab16Entries) return;
+  uint32_t sj[8] = {j, 0, 0, 0, 0, 0, 0, 0};
+  ge_p2 P;
+  ge_scalarmult_base(P, sj, tb);
+  ge_niels nj;
+  ge_p2_to_niels(nj, P);
+  int32_t w[32];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    w[k] = nj.ypx.v[k];
+    w[10 + k] = nj.ymx.v[k];
+    w[20 + k] = nj.xy2d.v[k];
+  }
+  w[30] = w[31] = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) out[(size_t)j * 8 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
 // ------------------------------------------------------------------ launchers (host side)
 
+size_t btab16_bytes() { return (size_t)kBtab16Entries * 8 * 16; }
+
+hipError_t launch_build_btab16(int4* out, hipStream_t stream) {
+  hipLaunchKernelGGL(build_btab16_kernel, dim3((kBtab16Entries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
-                         const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch, int grid,
-                         hipStream_t stream) {
+                         const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
+                         const int4* btab16, int grid, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t need_blocks = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
   hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                     verdicts, scratch);
+                     verdicts, scratch, btab16);
   return hipGetLastError();
 }
 

@@ -126,4 +126,22 @@ AT2V_HD AT2V_INLINE void sc_recode8(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-2^16 digits e_0..e_15 of a scalar < 2^253, e_i in [-2^15, 2^15), stored as (e_i + 2^15)
+// halfwords: word j holds digits 2j (low half) and 2j+1 (high half).
+AT2V_HD AT2V_INLINE void sc_recode16(uint32_t out[8], const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      int d = (int)((s[j] >> (16 * m)) & 0xffff) + carry;
+      carry = (d + 0x8000) >> 16;
+      d -= carry << 16;
+      w |= (uint32_t)(d + 0x8000) << (16 * m);
+    }
+    out[j] = w;
+  }
+}
+
 }  // namespace at2v

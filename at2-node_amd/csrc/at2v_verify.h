@@ -7,8 +7,9 @@
 // Double-scalar multiplication R' = [k](-A) + [s]B uses one shared doubling chain with
 // wavefront-uniform fixed windows (every lane adds at the same positions, no divergence):
 //   k : 64 signed radix-16 digits  in [-8, 8]     -> table [0..8](-A), cached form, per lane (global scratch)
-//   s : 32 signed radix-256 digits in [-128, 128] -> table [0..128]B, affine Niels, in LDS
-//   R = sum_i 16^i (k_i(-A) + [i even] s_{i/2} B), Horner from i = 63: 252 doublings, 64 + 32 additions.
+//   s : 16 signed radix-2^16 digits in [-2^15, 2^15] -> table [0..2^15]B, affine Niels, 4.2 MB in global
+//       memory (L2/MALL), entries prefetched into LDS by LDS-DMA
+//   R = sum_i 16^i (k_i(-A) + [4 | i] s_{i/4} B), Horner from i = 63: 252 doublings, 64 + 16 additions.
 // Any correct evaluation of [k](-A) + [s]B yields the same group element, so verdicts are
 // identical to dalek's NAF-5/NAF-8 vartime ladder (the oracle restates that one).
 #pragma once
@@ -49,13 +50,42 @@ AT2V_HD AT2V_INLINE int enc_small_order(const uint32_t s[8]) {
   return hit;
 }
 
+// [s]B for a reduced scalar s < l: Horner over 32 signed radix-256 digits, 8 doublings per digit
+template <class TabB>
+AT2V_HD AT2V_INLINE void ge_scalarmult_base(ge_p2& out, const uint32_t s[8], const TabB& tb) {
+  uint32_t sd[8];
+  sc_recode8(sd, s);
+  ge_p3 R3;
+  ge_p1p1 t;
+  ge_niels nb;
+  ge_p3_identity(R3);
+  ge_p2 R2;
+  for (int j = 31; j >= 0; --j) {
+    if (j != 31) {
+      for (int r = 0; r < 7; ++r) {
+        ge_p2_dbl(t, R2);
+        ge_p1p1_to_p2(R2, t);
+      }
+      ge_p2_dbl(t, R2);
+      ge_p1p1_to_p3(R3, t);
+    }
+    const int e = (int)((sd[j >> 2] >> (8 * (j & 3))) & 255) - 128;
+    tb.load(e < 0 ? -e : e, nb);
+    ge_niels_cneg(nb, e < 0);
+    ge_madd(t, R3, nb);
+    ge_p1p1_to_p2(R2, t);
+  }
+  out = R2;
+}
+
 // Table access policies.
 //   TabA: void store(int e, const ge_cached&); void load(int e, ge_cached&);  (per lane, e in 0..8)
 //         void prefetch(int e); void load_prefetched(ge_cached&)   (asynchronous load of one entry)
-//   TabB: void load(int e, ge_niels&)                                          (shared, e in 0..128)
-template <class TabA, class TabB, class MsgWord, class RLoad>
-AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
-                                    MsgWord msgword, int policy, TabA& ta, const TabB& tb, RLoad rload) {
+//   TabB: void prefetch(int e); void load_prefetched(ge_niels&)               (shared, e in 0..32768)
+// V1..V4: checks, decode, hash, ladder. Returns the checks' verdict; R' = [k](-A) + [s]B in Rp.
+template <class TabA, class TabB, class MsgWord>
+AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
+                                      uint32_t len, MsgWord msgword, int policy, TabA& ta, const TabB& tb) {
   // V1: s < l
   int ok = sc_is_canonical(Sw);
   if (policy == POLICY_LIBSODIUM_1_0_18) {
@@ -82,7 +112,7 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
   }
   uint32_t kd[8], sd[8];
   sc_recode4(kd, k);
-  sc_recode8(sd, Sw);
+  sc_recode16(sd, Sw);
 
   // table [j](-A), j = 0..8
   fe_neg(A.X, A.X);
@@ -119,7 +149,12 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
   }
   for (int i = 62; i >= 0; --i) {
     const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
-    ta.prefetch(d < 0 ? -d : d);  // lands while the four doublings run
+    ta.prefetch(d < 0 ? -d : d);  // both tables land while the window's four doublings run
+    int e = 0;
+    if ((i & 3) == 0) {  // s digit j = i/4 (radix 2^16) at every fourth radix-16 window
+      e = (int)((sel8(sd, i >> 3) >> (16 * ((i >> 2) & 1))) & 0xffff) - 0x8000;
+      tb.prefetch(e < 0 ? -e : e);
+    }
     for (int r = 0; r < 3; ++r) {
       ge_p2_dbl(t, R2);
       ge_p1p1_to_p2(R2, t);
@@ -129,23 +164,44 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
     ge_p1p1_to_p3(R3, t);
     ge_cached_cneg(ca, d < 0);
     ge_add(t, R3, ca);
-    if ((i & 1) == 0) {
-      const int e = (int)((sel8(sd, i >> 3) >> (8 * ((i >> 1) & 3))) & 255) - 128;
+    if ((i & 3) == 0) {
       ge_p1p1_to_p3(R3, t);
-      tb.load(e < 0 ? -e : e, nb);
+      tb.load_prefetched(nb);
       ge_niels_cneg(nb, e < 0);
       ge_madd(t, R3, nb);
     }
     ge_p1p1_to_p2(R2, t);
   }
-  // V5/V6: canonical encoding of R' == R bytes
-  uint32_t enc[8], Rr[8];
-  ge_p2_tobytes(enc, R2);
-  rload(Rr);  // R re-read at the end rather than kept live across the ladder
+  Rp = R2;
+  return ok;
+}
+
+// V5/V6: enc(R') with 1/Z given, compared with the 32 bytes of R (re-read by the caller, not kept live
+// across the ladder)
+AT2V_HD AT2V_INLINE int verify_finish(const ge_p2& Rp, const fe& zinv, const uint32_t Rr[8]) {
+  fe x, y;
+  fe_mul(x, Rp.X, zinv);
+  fe_mul(y, Rp.Y, zinv);
+  uint32_t enc[8], xb[8];
+  fe_tobytes(enc, y);
+  fe_tobytes(xb, x);
+  enc[7] ^= (xb[0] & 1u) << 31;
   int eq = 1;
 #pragma unroll
   for (int i = 0; i < 8; ++i) eq &= enc[i] == Rr[i];
-  return ok & eq;
+  return eq;
+}
+
+template <class TabA, class TabB, class MsgWord, class RLoad>
+AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                    MsgWord msgword, int policy, TabA& ta, const TabB& tb, RLoad rload) {
+  ge_p2 Rp;
+  const int ok = verify_ladder(Rp, Rw, Aw, Sw, len, msgword, policy, ta, tb);
+  fe zinv;
+  fe_invert(zinv, Rp.Z);
+  uint32_t Rr[8];
+  rload(Rr);
+  return ok & verify_finish(Rp, zinv, Rr);
 }
 
 }  // namespace at2v

@@ -18,7 +18,7 @@ struct HostTabA {
   void prefetch(int i) { pending = i; }
   void load_prefetched(ge_cached& c) const { c = e[pending]; }
 };
-struct HostTabB {
+struct HostTabB8 {
   void load(int i, ge_niels& n) const {
     const int32_t* p = &AT2V_BTAB[i * AT2V_BTAB_WORDS];
     for (int k = 0; k < 10; ++k) {
@@ -27,6 +27,28 @@ struct HostTabB {
       n.xy2d.v[k] = p[20 + k];
     }
   }
+};
+// [j]B, j = 0..2^15, built incrementally (P_j = P_{j-1} + B) and converted to affine Niels
+struct HostTabB16 {
+  std::vector<ge_niels> t;
+  mutable int pending = 0;
+  HostTabB16() {
+    t.resize((1 << 15) + 1);
+    ge_niels B1;
+    HostTabB8().load(1, B1);
+    ge_p3 P;
+    ge_p3_identity(P);
+    for (size_t j = 0; j < t.size(); ++j) {
+      ge_p2 q;
+      ge_p3_to_p2(q, P);
+      ge_p2_to_niels(t[j], q);
+      ge_p1p1 r;
+      ge_madd(r, P, B1);
+      ge_p1p1_to_p3(P, r);
+    }
+  }
+  void prefetch(int e) const { pending = e; }
+  void load_prefetched(ge_niels& n) const { n = t[pending]; }
 };
 
 static void words(uint32_t w[8], const uint8_t* b) {
@@ -59,8 +81,8 @@ int main(int argc, char** argv) {
       for (int b = 0; b < 4; ++b) if (4 * j + b < len) v |= (uint32_t)m[4 * j + b] << (8 * b);
       return v;
     };
+    static HostTabB16 tb;
     HostTabA ta;
-    HostTabB tb;
     auto rl = [&](uint32_t r[8]) { for (int q = 0; q < 8; ++q) r[q] = R[q]; };
     int d = verify_core(R, A, S, len, mw, POLICY_DALEK_V1, ta, tb, rl);
     int s = verify_core(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tb, rl);

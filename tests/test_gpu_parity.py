@@ -201,3 +201,14 @@ def test_multi_gpu_context_if_available(at2v_mod, golden):
     g = golden["adversarial"]
     assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek)
     v.close()
+
+
+def test_paired_chunks_adversarial(verifier, oracle):
+    """Enough records that every wave verifies chunk PAIRS (shared final inversion, Montgomery's trick):
+    > 2048 resident waves x 64 records. Adversarial mix, odd tail, compared record by record."""
+    n = (1 << 18) + 37
+    pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 2, 0, n, 64)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    got = verifier.verify_batch(pk, sig, msg, off)
+    assert np.array_equal(got, want), _mismatch(got, want, cls)
+    assert 0.85 * n < want.sum() < n
