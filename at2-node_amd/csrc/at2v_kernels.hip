@@ -3,10 +3,11 @@
 // Verify kernel layout:
 //   * one lane = one signature; a wave owns a contiguous chunk of 64 records, so the verdict bits of a
 //     chunk are one __ballot -> two uint32 words written by lane 0 (no atomics, no cross-wave traffic);
-//   * persistent grid (resident waves only), chunk = wave_id + k * total_waves; each wave reuses a fixed
-//     92 KiB slice of the scratch buffer for its 64 per-lane tables [0..8](-A) (cached form, 160 B each),
-//     lane-interleaved in 16-byte granules so a table store is one coalesced 1 KiB row per granule;
-//   * the fixed-base table [0..128]B (affine Niels, 128 B per entry) is staged once per workgroup in LDS;
+//   * persistent grid (resident waves only), chunks c = wave_id + k * total_waves taken in pairs that
+//     share one field inversion; each wave reuses a fixed 98 KiB slice of the scratch buffer for its 64
+//     per-lane tables [0..8](-A) (cached form, 160 B each, lane-contiguous) and the parked R' of a pair;
+//   * the fixed-base table [0..2^15]B (affine Niels, 128 B per entry, 4.2 MB) is built once per context
+//     and stays L2/MALL-resident; A and B entries reach the lanes through LDS-DMA prefetches;
 //   * records are read straight from the ABI layout (pk n x 32, sig n x 64, msg + offsets) with
 //     16-byte loads for A/R/S and 4-byte loads + v_alignbit for unaligned message words.
 #include <hip/hip_runtime.h>
@@ -172,6 +173,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     const int npair = c2 < nchunks ? 2 : 1;
     int ok0 = 0, ok1 = 0;
     ge_p2 Rp;
+    AT2V_PHASE(0);
 #pragma unroll 1
     for (int h = 0; h < npair; ++h) {
       const uint32_t chunk = h ? c2 : c;
@@ -222,6 +224,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
       R1 = Rp;
       fe_invert(zi1, Rp.Z);
     }
+    AT2V_PHASE(5);
 #pragma unroll 1
     for (int h = 0; h < npair; ++h) {
       const uint32_t chunk = h ? c2 : c;
@@ -236,6 +239,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
         if (2 * chunk + 1 < nwords) verdicts[2 * chunk + 1] = (uint32_t)(mask >> 32);
       }
     }
+    AT2V_PHASE(6);
   }
 }
 

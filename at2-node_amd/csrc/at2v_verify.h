@@ -17,6 +17,12 @@
 #include "at2v_sc.h"
 #include "at2v_sha512.h"
 
+// Phase-timing hook (tools/phase_bench.hip defines it to accumulate s_memtime deltas per wave; the
+// product build compiles it away).
+#ifndef AT2V_PHASE
+#define AT2V_PHASE(k)
+#endif
+
 namespace at2v {
 
 enum { POLICY_DALEK_V1 = 0, POLICY_LIBSODIUM_1_0_18 = 1 };
@@ -95,6 +101,7 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
   // V2: decode A (dalek rules)
   ge_p3 A;
   ok &= ge_frombytes(A, Aw);
+  AT2V_PHASE(1);
   // V3: k = SHA-512(R || A || M) mod l
   uint32_t k[8];
   {
@@ -113,6 +120,7 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
   uint32_t kd[8], sd[8];
   sc_recode4(kd, k);
   sc_recode16(sd, Sw);
+  AT2V_PHASE(2);
 
   // table [j](-A), j = 0..8
   fe_neg(A.X, A.X);
@@ -133,6 +141,7 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
     }
   }
 
+  AT2V_PHASE(3);
   // V4: shared doubling chain over 64 radix-16 windows
   ge_p2 R2;
   ge_p3 R3;
@@ -173,6 +182,7 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
     ge_p1p1_to_p2(R2, t);
   }
   Rp = R2;
+  AT2V_PHASE(4);
   return ok;
 }
 

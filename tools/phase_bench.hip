@@ -1,0 +1,96 @@
+// Phase breakdown of the verify kernel on gfx950: the product kernel (at2v_kernels.hip, included
+// verbatim) built with AT2V_PHASE(k) = "lane 0 adds the s_memtime delta since the previous mark to
+// bucket k of its wave". Buckets: 0 loop/pair overhead, 1 loads + V1 + decompress A, 2 SHA-512 + mod l +
+// recode, 3 A table, 4 ladder, 5 pair inversion, 6 encode + compare + verdict store.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I at2-node_amd/csrc tools/phase_bench.hip -o tools/phase_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define AT2V_MAX_WAVES 4096
+__device__ unsigned long long at2v_phase_acc[AT2V_MAX_WAVES][8];
+__device__ unsigned long long at2v_phase_last[AT2V_MAX_WAVES];
+__device__ __forceinline__ void at2v_phase_mark(int k) {
+  const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && w < AT2V_MAX_WAVES) {
+    const unsigned long long t = clock64();
+    if (k > 0) at2v_phase_acc[w][k] += t - at2v_phase_last[w];
+    else if (at2v_phase_last[w]) at2v_phase_acc[w][0] += t - at2v_phase_last[w];
+    at2v_phase_last[w] = t;
+  }
+}
+#define AT2V_PHASE(k) at2v_phase_mark(k)
+
+#include "at2v_kernels.hip"
+
+#define CHECK(x)                                                               \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      printf("HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return 1;                                                                \
+    }                                                                          \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 20);
+  const uint32_t L = 100;
+  hipDeviceProp_t prop;
+  CHECK(hipGetDeviceProperties(&prop, 0));
+  int bpc = 0, vg = 0;
+  CHECK(at2v::verify_occupancy(&bpc, &vg));
+  const int grid = prop.multiProcessorCount * bpc;
+  if (grid * 4 > AT2V_MAX_WAVES) {
+    printf("grid too large\n");
+    return 1;
+  }
+  uint8_t *pk, *sig, *msg;
+  uint32_t *off, *ver;
+  int4 *scratch, *btab;
+  CHECK(hipMalloc(&pk, (size_t)n * 32));
+  CHECK(hipMalloc(&sig, (size_t)n * 64));
+  CHECK(hipMalloc(&msg, (size_t)n * L));
+  CHECK(hipMalloc(&off, (size_t)(n + 1) * 4));
+  CHECK(hipMalloc(&ver, (size_t)(n + 31) / 32 * 4));
+  CHECK(hipMalloc(&scratch, (size_t)grid * at2v::scratch_bytes_per_block()));
+  CHECK(hipMalloc(&btab, at2v::btab16_bytes()));
+  CHECK(at2v::launch_build_btab16(btab, 0));
+  CHECK(at2v::launch_gen(0x4154325F, 0, n, L, pk, sig, msg, off, 0));
+  CHECK(hipDeviceSynchronize());
+  std::vector<unsigned long long> zero(AT2V_MAX_WAVES * 8, 0), zl(AT2V_MAX_WAVES, 0);
+  float ms = 0;
+  for (int rep = 0; rep < 2; ++rep) {
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_acc), zero.data(), zero.size() * 8));
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_last), zl.data(), zl.size() * 8));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventRecord(e0, 0));
+    CHECK(at2v::launch_verify(pk, sig, msg, n * L, off, n, 0, ver, scratch, btab, grid, 0));
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+  }
+  std::vector<unsigned long long> acc(AT2V_MAX_WAVES * 8);
+  CHECK(hipMemcpyFromSymbol(acc.data(), HIP_SYMBOL(at2v_phase_acc), acc.size() * 8));
+  std::vector<uint32_t> hv((n + 31) / 32);
+  CHECK(hipMemcpy(hv.data(), ver, hv.size() * 4, hipMemcpyDeviceToHost));
+  size_t valid = 0;
+  for (uint32_t i = 0; i < n; ++i) valid += (hv[i / 32] >> (i % 32)) & 1;
+  const char* names[8] = {"pair/loop overhead", "loads+V1+decompress", "sha512+mod l+recode", "A table",
+                          "ladder", "pair inversion", "encode+compare+store", "-"};
+  double tot = 0, b[8] = {0};
+  const int waves = grid * 4;
+  for (int w = 0; w < waves; ++w)
+    for (int k = 0; k < 8; ++k) b[k] += (double)acc[w * 8 + k];
+  for (int k = 0; k < 8; ++k) tot += b[k];
+  printf("n=%u grid=%d waves=%d kernel %.3f ms -> %.2f M verifies/s, valid %zu/%u\n", n, grid, waves, ms,
+         n / ms / 1e3, valid, n);
+  const double chunks = (double)n / 64;
+  for (int k = 0; k < 7; ++k)
+    printf("  %-24s %6.2f %%   %10.0f wave-cycles per 64-record chunk\n", names[k], 100 * b[k] / tot, b[k] / chunks);
+  printf("  total                    %10.0f wave-cycles per chunk (s_memtime; 2 waves share a SIMD)\n", tot / chunks);
+  return valid == n ? 0 : 2;
+}
