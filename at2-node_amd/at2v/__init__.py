@@ -30,7 +30,13 @@ _POLICIES = {"dalek": POLICY_DALEK_V1, "dalek_v1": POLICY_DALEK_V1, "libsodium":
 # must match include/at2v.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = ("at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
                     "at2v_verify_one", "at2v_strerror", "at2v_gen_records_device", "at2v_sign_batch",
-                    "at2v_get_info")
+                    "at2v_get_info", "at2v_decode_points",
+                    "at2v_queue_create", "at2v_queue_destroy", "at2v_queue_submit", "at2v_queue_flush",
+                    "at2v_queue_poll", "at2v_queue_get_stats", "at2v_queue_reset_latency",
+                    "at2v_pack_send_asset",
+                    "at2v_ledger_create", "at2v_ledger_destroy", "at2v_ledger_balance", "at2v_ledger_last_sequence",
+                    "at2v_ledger_transfer", "at2v_ledger_recent_put", "at2v_ledger_recent_get",
+                    "at2v_ledger_deliver", "at2v_ledger_pending")
 
 
 class At2vError(RuntimeError):
@@ -90,6 +96,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.at2v_sign_batch.restype = ctypes.c_int
     lib.at2v_get_info.argtypes = [P, ctypes.POINTER(_Info)]
     lib.at2v_get_info.restype = ctypes.c_int
+    lib.at2v_decode_points.argtypes = [P, P, ctypes.c_size_t, P]
+    lib.at2v_decode_points.restype = ctypes.c_int
+    from . import node as _node  # queue / packer / ledger signatures
+    _node.bind(lib)
     _lib = lib
     return lib
 
@@ -187,6 +197,14 @@ class BatchVerifier:
                            d_off: Optional[int], stream: int = 0) -> None:
         _check(self._lib.at2v_gen_records_device(self._h, cfg_seed, first, n, msg_len, d_pk, d_sig, d_msg,
                                                  d_off or None, stream or None), "at2v_gen_records_device")
+
+    def decode_points(self, pts: np.ndarray) -> np.ndarray:
+        """bool[n]: 32-byte encodings that decode under dalek rules (GPU kernel)"""
+        pts = np.ascontiguousarray(pts, dtype=np.uint8).reshape(-1, 32)
+        n = len(pts)
+        words = np.zeros(max(1, (n + 31) // 32), dtype=np.uint32)
+        _check(self._lib.at2v_decode_points(self._h, _ptr(pts), n, _ptr(words)), "at2v_decode_points")
+        return unpack_verdicts(words, n)
 
     def sign_batch(self, seeds: np.ndarray, msg: np.ndarray, msg_off: np.ndarray):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint8)

@@ -25,6 +25,7 @@ hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len
                       uint8_t* msg, uint32_t* off, hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_total, const uint32_t* off, uint32_t n,
                        uint8_t* pk, uint8_t* sig, hipStream_t stream);
+hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStream_t stream);
 hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs);
 size_t scratch_bytes_per_block();
 int block_threads();
@@ -327,6 +328,25 @@ int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, con
   doff.release();
   dpk.release();
   dsig.release();
+  (void)hipSetDevice(prev);
+  return hip_code(e);
+}
+
+int at2v_decode_points(at2v_ctx* ctx, const uint8_t* pts, size_t n, uint32_t* valid_words) {
+  if (!ctx) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!pts || !valid_words || n >= (1u << 31)) return AT2V_E_INVALID;
+  Shard& s = ctx->shards[0];
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  const size_t words = (n + 31) / 32;
+  hipError_t e = hipSetDevice(s.device);
+  if (e == hipSuccess) e = s.pk.ensure(n * 32);
+  if (e == hipSuccess) e = s.verdict.ensure(words * 4);
+  if (e == hipSuccess) e = hipMemcpyAsync(s.pk.p, pts, n * 32, hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess) e = at2v::launch_decode((const uint8_t*)s.pk.p, (uint32_t)n, (uint32_t*)s.verdict.p, s.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(valid_words, s.verdict.p, words * 4, hipMemcpyDeviceToHost, s.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
   (void)hipSetDevice(prev);
   return hip_code(e);
 }

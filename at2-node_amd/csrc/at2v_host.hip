@@ -1,0 +1,314 @@
+// at2v_host.hip — C ABI of the host-side pieces around the verify kernel (include/at2v.h):
+//   * at2v_queue_*   ingest/batching queue (at2v_queue.h) over a HIP backend: pinned host slots, one
+//                    stream each for H2D copies, verify kernels and D2H copies, so batch k+1 uploads while
+//                    batch k verifies (kernels themselves serialise: they share the context's scratch);
+//   * at2v_pack_*    SendAssetRequest -> verify records (at2v_pack.h);
+//   * at2v_ledger_*  accounts / recent transactions / apply loop (at2v_ledger.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+
+#include "../../include/at2v.h"
+#include "at2v_ledger.h"
+#include "at2v_pack.h"
+#include "at2v_queue.h"
+
+namespace {
+
+struct DevSlot {
+  void *pk = nullptr, *sig = nullptr, *msg = nullptr, *off = nullptr, *ver = nullptr;
+  hipEvent_t uploaded = nullptr, verified = nullptr, done = nullptr;
+};
+
+struct HipBackend {
+  at2v_ctx* ctx = nullptr;
+  int device = 0;
+  hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+
+  int init(const at2v_queue_opts& o) {
+    at2v_opts co{o.device, 1, o.policy};
+    const int rc = at2v_create(&co, &ctx);
+    if (rc) return rc;
+    device = o.device;
+    if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
+    if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
+    if (hipStreamCreateWithFlags(&comp, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
+    if (hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
+    return AT2V_OK;
+  }
+  void fini() {
+    if (hipSetDevice(device) == hipSuccess) {
+      for (hipStream_t* s : {&h2d, &comp, &d2h})
+        if (*s) {
+          (void)hipStreamSynchronize(*s);
+          (void)hipStreamDestroy(*s);
+          *s = nullptr;
+        }
+    }
+    at2v_destroy(ctx);
+    ctx = nullptr;
+  }
+
+  int alloc(at2v::QueueSlot& s) {
+    if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
+    DevSlot* d = new (std::nothrow) DevSlot;
+    if (!d) return AT2V_E_OOM;
+    s.backend = d;
+    const size_t words = (s.cap_records + 31) / 32;
+    bool ok = hipHostMalloc((void**)&s.pk, s.cap_records * 32, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&s.sig, s.cap_records * 64, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&s.msg, s.cap_msg, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&s.off, (s.cap_records + 1) * 4, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void**)&s.verdicts, words * 4, hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&d->pk, s.cap_records * 32) == hipSuccess && hipMalloc(&d->sig, s.cap_records * 64) == hipSuccess &&
+              hipMalloc(&d->msg, s.cap_msg + 16) == hipSuccess && hipMalloc(&d->off, (s.cap_records + 1) * 4) == hipSuccess &&
+              hipMalloc(&d->ver, words * 4) == hipSuccess &&
+              hipEventCreateWithFlags(&d->uploaded, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&d->verified, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&d->done, hipEventDisableTiming) == hipSuccess;
+    return ok ? AT2V_OK : AT2V_E_OOM;
+  }
+  void release(at2v::QueueSlot& s) {
+    (void)hipSetDevice(device);
+    for (void* p : {(void*)s.pk, (void*)s.sig, (void*)s.msg, (void*)s.off, (void*)s.verdicts})
+      if (p) (void)hipHostFree(p);
+    s.pk = s.sig = s.msg = nullptr;
+    s.off = s.verdicts = nullptr;
+    DevSlot* d = static_cast<DevSlot*>(s.backend);
+    if (!d) return;
+    for (void* p : {d->pk, d->sig, d->msg, d->off, d->ver})
+      if (p) (void)hipFree(p);
+    for (hipEvent_t e : {d->uploaded, d->verified, d->done})
+      if (e) (void)hipEventDestroy(e);
+    delete d;
+    s.backend = nullptr;
+  }
+  // H2D on h2d -> verify on comp (waits for its upload) -> D2H on d2h (waits for its kernel)
+  int launch(at2v::QueueSlot& s) {
+    DevSlot* d = static_cast<DevSlot*>(s.backend);
+    hipError_t e = hipSetDevice(device);
+    const size_t n = s.n, words = (n + 31) / 32;
+    if (e == hipSuccess) e = hipMemcpyAsync(d->pk, s.pk, n * 32, hipMemcpyHostToDevice, h2d);
+    if (e == hipSuccess) e = hipMemcpyAsync(d->sig, s.sig, n * 64, hipMemcpyHostToDevice, h2d);
+    if (e == hipSuccess && s.msg_used) e = hipMemcpyAsync(d->msg, s.msg, s.msg_used, hipMemcpyHostToDevice, h2d);
+    if (e == hipSuccess) e = hipMemcpyAsync(d->off, s.off, (n + 1) * 4, hipMemcpyHostToDevice, h2d);
+    if (e == hipSuccess) e = hipEventRecord(d->uploaded, h2d);
+    if (e == hipSuccess) e = hipStreamWaitEvent(comp, d->uploaded, 0);
+    if (e != hipSuccess) return AT2V_E_HIP;
+    const int rc = at2v_verify_batch_device(ctx, (const uint8_t*)d->pk, (const uint8_t*)d->sig, (const uint8_t*)d->msg,
+                                            s.msg_used, (const uint32_t*)d->off, n, (uint32_t*)d->ver, comp);
+    if (rc) return rc;
+    e = hipEventRecord(d->verified, comp);
+    if (e == hipSuccess) e = hipStreamWaitEvent(d2h, d->verified, 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.verdicts, d->ver, words * 4, hipMemcpyDeviceToHost, d2h);
+    if (e == hipSuccess) e = hipEventRecord(d->done, d2h);
+    return e == hipSuccess ? AT2V_OK : AT2V_E_HIP;
+  }
+  int wait(at2v::QueueSlot& s) {
+    DevSlot* d = static_cast<DevSlot*>(s.backend);
+    return hipEventSynchronize(d->done) == hipSuccess ? AT2V_OK : AT2V_E_HIP;
+  }
+};
+
+}  // namespace
+
+struct at2v_queue {
+  HipBackend be;
+  at2v::BatchQueue<HipBackend>* q = nullptr;
+};
+
+struct at2v_ledger {
+  at2v::Ledger l;
+};
+
+extern "C" {
+
+int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
+  if (!out) return AT2V_E_INVALID;
+  *out = nullptr;
+  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0};
+  if (opts) o = *opts;
+  at2v::QueueOpts qo;
+  if (o.max_batch) qo.max_batch = o.max_batch;
+  if (o.max_delay_us) qo.max_delay_us = o.max_delay_us;
+  if (o.max_msg_bytes) qo.max_msg_bytes = o.max_msg_bytes;
+  if (o.depth) qo.depth = (int)o.depth;
+  if (qo.depth < 2 || qo.max_batch >= (1u << 31) || (uint64_t)qo.max_batch * qo.max_msg_bytes >= (1ull << 32))
+    return AT2V_E_INVALID;
+  at2v_queue* q = new (std::nothrow) at2v_queue;
+  if (!q) return AT2V_E_OOM;
+  int rc = q->be.init(o);
+  if (rc == AT2V_OK) {
+    q->q = new (std::nothrow) at2v::BatchQueue<HipBackend>(q->be, qo);
+    rc = q->q ? q->q->start() : AT2V_E_OOM;
+  }
+  if (rc != AT2V_OK) {
+    at2v_queue_destroy(q);
+    return rc < 0 ? rc : AT2V_E_HIP;
+  }
+  *out = q;
+  return AT2V_OK;
+}
+
+void at2v_queue_destroy(at2v_queue* q) {
+  if (!q) return;
+  delete q->q;  // stop(): seal, complete, join, free the slots
+  q->be.fini();
+  delete q;
+}
+
+int at2v_queue_submit(at2v_queue* q, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                      const uint32_t* msg_off, size_t n, uint64_t* first_ticket) {
+  if (!q || !q->q) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!pk || !sig || !msg_off || (!msg && msg_off[n] != msg_off[0])) return AT2V_E_INVALID;
+  return q->q->submit(pk, sig, msg, msg_off, n, first_ticket) == 0 ? AT2V_OK : AT2V_E_INVALID;
+}
+
+int at2v_queue_flush(at2v_queue* q) {
+  if (!q || !q->q) return AT2V_E_INVALID;
+  q->q->flush();
+  return AT2V_OK;
+}
+
+long at2v_queue_poll(at2v_queue* q, uint64_t* tickets, uint8_t* verdicts, size_t max, uint32_t timeout_us) {
+  if (!q || !q->q || (max && (!tickets || !verdicts))) return AT2V_E_INVALID;
+  return q->q->poll(tickets, verdicts, max, timeout_us);
+}
+
+int at2v_queue_get_stats(at2v_queue* q, at2v_queue_stats* out) {
+  if (!q || !q->q || !out) return AT2V_E_INVALID;
+  const at2v::QueueStats s = q->q->stats();
+  out->submitted = s.submitted;
+  out->completed = s.completed;
+  out->batches = s.batches;
+  out->failed_batches = s.failed_batches;
+  out->mean_batch = s.mean_batch;
+  out->p50_us = s.p50_us;
+  out->p99_us = s.p99_us;
+  out->max_us = s.max_us;
+  return AT2V_OK;
+}
+
+int at2v_queue_reset_latency(at2v_queue* q) {
+  if (!q || !q->q) return AT2V_E_INVALID;
+  q->q->reset_latency();
+  return AT2V_OK;
+}
+
+long at2v_pack_send_asset(const at2v_send_asset_request* req, size_t n, int wire, uint8_t* pk_out, uint8_t* sig_out,
+                          uint8_t* msg_out, uint32_t* msg_off_out, uint8_t* recipient_out, uint8_t* status_out) {
+  if (n && (!req || !pk_out || !sig_out || !msg_out || !msg_off_out || !recipient_out || !status_out))
+    return AT2V_E_INVALID;
+  if (wire != AT2V_WIRE_BYTES && wire != AT2V_WIRE_ARRAY) return AT2V_E_INVALID;
+  if (!msg_off_out) return AT2V_E_INVALID;
+  long ok = 0;
+  uint32_t o = 0;
+  msg_off_out[0] = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const at2v_send_asset_request& r = req[i];
+    // rpc.rs order: recipient (:265), sender (:269), signature (:281)
+    const uint8_t* rcp = at2v::wire_field(r.recipient, r.recipient_len, 32, wire);
+    const uint8_t* snd = rcp ? at2v::wire_field(r.sender, r.sender_len, 32, wire) : nullptr;
+    const uint8_t* sg = snd ? at2v::wire_field(r.signature, r.signature_len, 64, wire) : nullptr;
+    const uint8_t st = !rcp ? AT2V_PACK_BAD_RECIPIENT : !snd ? AT2V_PACK_BAD_SENDER : !sg ? AT2V_PACK_BAD_SIGNATURE
+                                                                                           : AT2V_PACK_OK;
+    status_out[i] = st;
+    if (st == AT2V_PACK_OK) {
+      std::memcpy(pk_out + 32 * i, snd, 32);
+      std::memcpy(sig_out + 64 * i, sg, 64);
+      std::memcpy(recipient_out + 32 * i, rcp, 32);
+      o += (uint32_t)at2v::thin_transaction(msg_out + o, rcp, r.amount, wire);
+      ++ok;
+    } else {
+      std::memset(pk_out + 32 * i, 0, 32);
+      std::memset(sig_out + 64 * i, 0, 64);
+      std::memset(recipient_out + 32 * i, 0, 32);
+    }
+    msg_off_out[i + 1] = o;
+  }
+  return ok;
+}
+
+int at2v_ledger_create(at2v_ledger** out) {
+  if (!out) return AT2V_E_INVALID;
+  *out = new (std::nothrow) at2v_ledger;
+  return *out ? AT2V_OK : AT2V_E_OOM;
+}
+
+void at2v_ledger_destroy(at2v_ledger* l) { delete l; }
+
+int at2v_ledger_balance(const at2v_ledger* l, const uint8_t pk[32], uint64_t* out) {
+  if (!l || !pk || !out) return AT2V_E_INVALID;
+  *out = l->l.balance(at2v::make_key(pk));
+  return AT2V_OK;
+}
+
+int at2v_ledger_last_sequence(const at2v_ledger* l, const uint8_t pk[32], uint32_t* out) {
+  if (!l || !pk || !out) return AT2V_E_INVALID;
+  *out = l->l.last_sequence(at2v::make_key(pk));
+  return AT2V_OK;
+}
+
+int at2v_ledger_transfer(at2v_ledger* l, const uint8_t sender[32], uint32_t sequence, const uint8_t recipient[32],
+                         uint64_t amount) {
+  if (!l || !sender || !recipient) return AT2V_E_INVALID;
+  return l->l.transfer(at2v::make_key(sender), sequence, at2v::make_key(recipient), amount);
+}
+
+int at2v_ledger_recent_put(at2v_ledger* l, const uint8_t sender[32], uint32_t sequence, const uint8_t recipient[32],
+                           uint64_t amount, uint64_t now_us) {
+  if (!l || !sender || !recipient) return AT2V_E_INVALID;
+  l->l.recent_put(at2v::make_key(sender), sequence, at2v::make_key(recipient), amount, now_us);
+  return AT2V_OK;
+}
+
+long at2v_ledger_recent_get(const at2v_ledger* l, at2v_full_transaction* out, size_t max) {
+  if (!l || (max && !out)) return AT2V_E_INVALID;
+  long k = 0;
+  for (const auto& t : l->l.recent()) {
+    if ((size_t)k == max) break;
+    at2v_full_transaction& o = out[k++];
+    o.timestamp_us = t.timestamp_us;
+    std::memcpy(o.sender, t.sender.data(), 32);
+    o.sender_sequence = t.sender_sequence;
+    std::memcpy(o.recipient, t.recipient.data(), 32);
+    o.amount = t.amount;
+    o.state = t.state;
+  }
+  return k;
+}
+
+int at2v_ledger_deliver(at2v_ledger* l, const uint8_t* sender, const uint32_t* sequence, const uint8_t* recipient,
+                        const uint64_t* amount, const uint32_t* verdicts, size_t n, uint64_t now_us,
+                        at2v_apply_stats* stats) {
+  if (!l || (n && (!sender || !sequence || !recipient || !amount))) return AT2V_E_INVALID;
+  std::vector<at2v::Payload> batch;
+  batch.reserve(n);
+  uint64_t rejected = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (verdicts && !((verdicts[i >> 5] >> (i & 31)) & 1u)) {
+      ++rejected;
+      continue;
+    }
+    batch.push_back(at2v::Payload{sequence[i], at2v::make_key(sender + 32 * i), at2v::make_key(recipient + 32 * i),
+                                  amount[i], now_us, 0});
+  }
+  at2v::ApplyStats st;
+  st.rejected = rejected;
+  l->l.deliver(batch, now_us, &st);
+  if (stats) {
+    stats->delivered = batch.size();
+    stats->rejected = st.rejected;
+    stats->applied = st.applied;
+    stats->requeued = st.requeued;
+    stats->expired = st.expired;
+    stats->passes = st.passes;
+  }
+  return AT2V_OK;
+}
+
+long at2v_ledger_pending(const at2v_ledger* l) { return l ? (long)l->l.pending() : AT2V_E_INVALID; }
+
+}  // extern "C"

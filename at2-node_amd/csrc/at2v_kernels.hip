@@ -451,6 +451,26 @@ __global__ __launch_bounds__(kBlock) void build_btab16_kernel(int4* __restrict__
   for (int q = 0; q < 8; ++q) out[(size_t)j * 8 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
+// dalek CompressedEdwardsY::decompress success bit per 32-byte point (at2v_decode_points): one lane per
+// point, verdict words written per wave like the verify kernel
+__global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restrict__ pts, uint32_t n,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  int ok = 0;
+  if (i < n) {
+    uint32_t w[8];
+    load8(w, pts + (size_t)i * 32);
+    ge_p3 P;
+    ok = ge_frombytes(P, w);
+  }
+  const uint64_t mask = __ballot(ok);
+  const uint32_t first = i & ~63u, nwords = (n + 31) / 32;
+  if ((threadIdx.x & 63) == 0 && first < n) {
+    out[first / 32] = (uint32_t)mask;
+    if (first / 32 + 1 < nwords) out[first / 32 + 1] = (uint32_t)(mask >> 32);
+  }
+}
+
 // ------------------------------------------------------------------ launchers (host side)
 
 size_t btab16_bytes() { return (size_t)kBtab16Entries * 8 * 16; }
@@ -485,6 +505,12 @@ hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_to
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(sign_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, seeds, msg, msg_total, off,
                      n, pk, sig);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, pts, n, out);
   return hipGetLastError();
 }
 

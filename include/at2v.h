@@ -108,6 +108,111 @@ typedef struct {
 } at2v_info;
 int at2v_get_info(at2v_ctx* ctx, at2v_info* out);
 
+
+/* ---- ingest/batching queue: the server's verify call site ----
+ * Replaces the per-payload verify that sieve/murmur run on num_cpus::get() workers (rpc.rs:125,
+ * rpc.rs:275-284 -> rpc.rs:156). Producers submit records; a batch is sealed at max_batch records, when
+ * its oldest record is max_delay_us old, or on at2v_queue_flush(), and verified on the GPU
+ * asynchronously (depth slots: one filling, up to depth-1 in flight). Verdicts come back in ticket
+ * (= submission) order. Thread-safe: any number of producer threads; poll from any thread. */
+typedef struct at2v_queue at2v_queue;
+typedef struct {
+  int device;             /* HIP device ordinal */
+  at2v_policy policy;
+  uint32_t max_batch;     /* records per batch; 0 = 65536 */
+  uint32_t max_delay_us;  /* deadline of the oldest pending record; 0 = 1000 */
+  uint32_t max_msg_bytes; /* message bytes budgeted per record (slot capacity max_batch x this); 0 = 256 */
+  uint32_t depth;         /* batch slots, >= 2; 0 = 3 */
+} at2v_queue_opts;
+typedef struct {
+  uint64_t submitted, completed, batches, failed_batches;
+  double mean_batch;           /* records per completed batch */
+  double p50_us, p99_us, max_us; /* submit -> verdict published, per record (since create / reset) */
+} at2v_queue_stats;
+int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out);
+void at2v_queue_destroy(at2v_queue* q); /* seals and completes everything submitted, then frees */
+/* n records in the at2v_verify_batch layout; *first_ticket receives the ticket of record 0 (the call's
+ * records get consecutive tickets). Blocks only while every slot is busy (backpressure). */
+int at2v_queue_submit(at2v_queue* q, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                      const uint32_t* msg_off, size_t n, uint64_t* first_ticket);
+int at2v_queue_flush(at2v_queue* q);
+/* Up to max completed (ticket, verdict) pairs in ticket order, waiting up to timeout_us for the first.
+ * verdict: 1 valid, 0 invalid, 0xff the batch failed on the device. Returns the count (>= 0) or < 0. */
+long at2v_queue_poll(at2v_queue* q, uint64_t* tickets, uint8_t* verdicts, size_t max, uint32_t timeout_us);
+int at2v_queue_get_stats(at2v_queue* q, at2v_queue_stats* out);
+int at2v_queue_reset_latency(at2v_queue* q);
+
+/* ---- record packer: SendAssetRequest fields -> verify records ----
+ * Mirrors the server's decode of SendAssetRequest (at2.proto:10-16) at rpc.rs:264-281: recipient, then
+ * sender, then signature, each bincode-decoded; M = bincode(ThinTransaction{recipient, amount})
+ * (src/lib.rs:14-22, signed at src/client.rs:77-78). `wire` selects how drop's PublicKey/Signature
+ * serialise (not in the tree): AT2V_WIRE_BYTES = u64le length prefix + bytes (default assumption),
+ * AT2V_WIRE_ARRAY = raw bytes. Curve-point validity is NOT checked here (at2v_decode_points, and V2 of
+ * the verify kernel for the sender). */
+typedef struct {
+  const uint8_t* sender;
+  size_t sender_len;
+  uint32_t sequence;
+  const uint8_t* recipient;
+  size_t recipient_len;
+  uint64_t amount;
+  const uint8_t* signature;
+  size_t signature_len;
+} at2v_send_asset_request;
+enum { AT2V_WIRE_BYTES = 0, AT2V_WIRE_ARRAY = 1 };
+enum { AT2V_PACK_OK = 0, AT2V_PACK_BAD_RECIPIENT = 1, AT2V_PACK_BAD_SENDER = 2, AT2V_PACK_BAD_SIGNATURE = 3 };
+/* pk_out n x 32, sig_out n x 64, recipient_out n x 32, msg_out n x (48 | 40) bytes, msg_off_out n + 1,
+ * status_out n. A record that fails to decode keeps its index (zero key/signature, empty message).
+ * Returns the number of records with status AT2V_PACK_OK, or < 0. */
+long at2v_pack_send_asset(const at2v_send_asset_request* req, size_t n, int wire, uint8_t* pk_out, uint8_t* sig_out,
+                          uint8_t* msg_out, uint32_t* msg_off_out, uint8_t* recipient_out, uint8_t* status_out);
+
+/* Curve-point decoding on the GPU: bit i of valid_words = 1 iff pts[i] (32 bytes) decodes under
+ * curve25519-dalek CompressedEdwardsY::decompress — what bincode-deserialising a
+ * drop PublicKey checks at rpc.rs:265/269. Host buffers, synchronous, ctx's first device. */
+int at2v_decode_points(at2v_ctx* ctx, const uint8_t* pts, size_t n, uint32_t* valid_words);
+
+/* ---- ledger apply: what the server does with verified payloads ----
+ * Accounts (accounts/mod.rs, account.rs), the 10-entry recent-transactions log (recent_transactions.rs)
+ * and the deliver/apply loop of Service::spawn (rpc.rs:149-211), with the reference's quirks: an
+ * Underflow still consumes the sequence, every account error is retried, payloads are processed in
+ * descending (sequence, sender, recipient, amount) order per pass, TTL expiry (60 s) marks Failure but
+ * does not skip processing. Not thread-safe. */
+typedef struct at2v_ledger at2v_ledger;
+enum { AT2V_TX_OK = 0, AT2V_TX_INCONSECUTIVE_SEQUENCE = 1, AT2V_TX_OVERFLOW = 2, AT2V_TX_UNDERFLOW = 3 };
+enum { AT2V_TX_PENDING = 0, AT2V_TX_SUCCESS = 1, AT2V_TX_FAILURE = 2 };
+typedef struct {
+  uint64_t timestamp_us;
+  uint8_t sender[32];
+  uint32_t sender_sequence;
+  uint8_t recipient[32];
+  uint64_t amount;
+  int32_t state; /* AT2V_TX_PENDING / SUCCESS / FAILURE */
+} at2v_full_transaction;
+typedef struct {
+  uint64_t delivered; /* records whose verdict bit was 1 */
+  uint64_t rejected;  /* records whose verdict bit was 0 (never delivered) */
+  uint64_t applied;   /* transfers that succeeded during this call */
+  uint64_t requeued;  /* payloads still pending after the call (account errors are retried later) */
+  uint64_t expired;   /* TTL-expired payloads marked Failure during this call */
+  uint64_t passes;    /* passes of the apply loop */
+} at2v_apply_stats;
+int at2v_ledger_create(at2v_ledger** out);
+void at2v_ledger_destroy(at2v_ledger* l);
+int at2v_ledger_balance(const at2v_ledger* l, const uint8_t pk[32], uint64_t* out);
+int at2v_ledger_last_sequence(const at2v_ledger* l, const uint8_t pk[32], uint32_t* out);
+/* AccountsHandler::transfer: returns AT2V_TX_OK or an AT2V_TX_* error (>0), < 0 on bad arguments. */
+int at2v_ledger_transfer(at2v_ledger* l, const uint8_t sender[32], uint32_t sequence, const uint8_t recipient[32],
+                         uint64_t amount);
+int at2v_ledger_recent_put(at2v_ledger* l, const uint8_t sender[32], uint32_t sequence, const uint8_t recipient[32],
+                           uint64_t amount, uint64_t now_us);
+long at2v_ledger_recent_get(const at2v_ledger* l, at2v_full_transaction* out, size_t max);
+/* One delivered batch: records i with verdict bit i set (verdicts NULL = all) enter the apply loop. */
+int at2v_ledger_deliver(at2v_ledger* l, const uint8_t* sender, const uint32_t* sequence, const uint8_t* recipient,
+                        const uint64_t* amount, const uint32_t* verdicts, size_t n, uint64_t now_us,
+                        at2v_apply_stats* stats);
+long at2v_ledger_pending(const at2v_ledger* l);
+
 #ifdef __cplusplus
 }
 #endif
