@@ -18,9 +18,9 @@
 namespace at2v {
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab16, int grid, hipStream_t stream);
-size_t btab16_bytes();
-hipError_t launch_build_btab16(int4* out, hipStream_t stream);
+                         const int4* btab, int grid, hipStream_t stream);
+size_t btab_bytes();
+hipError_t launch_build_btab(int4* out, hipStream_t stream);
 hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint8_t* pk, uint8_t* sig,
                       uint8_t* msg, uint32_t* off, hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_total, const uint32_t* off, uint32_t n,
@@ -60,7 +60,7 @@ struct Shard {
   int cus = 0;
   int blocks_per_cu = 0;
   int vgprs = 0;
-  DevBuf scratch, btab16, pk, sig, msg, off, verdict;
+  DevBuf scratch, btab, pk, sig, msg, off, verdict;
 };
 
 }  // namespace
@@ -97,9 +97,9 @@ int init_shard(Shard& s, int device) {
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   AT2V_TRY(s.scratch.ensure((size_t)s.grid * at2v::scratch_bytes_per_block()));
-  // fixed-base table [0..2^15]B, built on the device once per context
-  AT2V_TRY(s.btab16.ensure(at2v::btab16_bytes()));
-  AT2V_TRY(at2v::launch_build_btab16((int4*)s.btab16.p, s.stream));
+  // fixed-base table [0..2^(AT2V_BWIN-1)]B, built on the device once per context
+  AT2V_TRY(s.btab.ensure(at2v::btab_bytes()));
+  AT2V_TRY(at2v::launch_build_btab((int4*)s.btab.p, s.stream));
   AT2V_TRY(hipStreamSynchronize(s.stream));
   return AT2V_OK;
 }
@@ -145,7 +145,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     s.scratch.release();
-    s.btab16.release();
+    s.btab.release();
     s.pk.release();
     s.sig.release();
     s.msg.release();
@@ -203,7 +203,7 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     if (e == hipSuccess)
       e = at2v::launch_verify((const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
                               (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (int)ctx->policy,
-                              (uint32_t*)s.verdict.p, (int4*)s.scratch.p, (const int4*)s.btab16.p, s.grid, s.stream);
+                              (uint32_t*)s.verdict.p, (int4*)s.scratch.p, (const int4*)s.btab.p, s.grid, s.stream);
     // a = multiple of 64 => the shard's words start at word a/32
     if (e == hipSuccess)
       e = hipMemcpyAsync(verdicts + a / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, s.stream);
@@ -235,7 +235,7 @@ int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* 
   hipError_t e = hipSetDevice(s.device);
   if (e == hipSuccess)
     e = at2v::launch_verify(d_pk, d_sig, d_msg, (uint32_t)msg_bytes, d_msg_off, (uint32_t)n, (int)ctx->policy,
-                            d_verdicts, (int4*)s.scratch.p, (const int4*)s.btab16.p, s.grid, (hipStream_t)hip_stream);
+                            d_verdicts, (int4*)s.scratch.p, (const int4*)s.btab.p, s.grid, (hipStream_t)hip_stream);
   (void)hipSetDevice(prev);
   return hip_code(e);
 }

@@ -20,11 +20,22 @@ namespace at2v {
 #define AT2V_VERIFY_WAVES_PER_SIMD 2  // register budget: 512 / waves VGPR+AGPR per lane
 #endif
 
+#ifndef AT2V_BWIN
+#define AT2V_BWIN 16  // fixed-base window bits: table [0..2^(AT2V_BWIN-1)]B
+#endif
+#ifndef AT2V_INV_GROUP
+#define AT2V_INV_GROUP 2  // chunks whose final inversions share one field inversion (Montgomery's trick)
+#endif
+
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kTabAGranules = 9 * 10;  // 9 entries x 10 x 16 B
-constexpr int kParkGranules = 8;       // parked R' (X, Y, Z: 30 words) of the first chunk of a pair
-constexpr int kLaneGranules = kTabAGranules + kParkGranules;
+constexpr int kBWin = AT2V_BWIN;
+constexpr int kGroup = AT2V_INV_GROUP;
+static_assert(kGroup >= 1 && kGroup <= 8, "inversion group");
+constexpr int kTabAGranules = 9 * 10;            // 9 entries x 10 x 16 B
+constexpr int kParkGranules = 8 * kGroup;        // parked R' (X, Y, Z: 30 words) of every chunk of a group
+constexpr int kPrefGranules = 3 * (kGroup - 1);  // prefix products Z_0..Z_h of the group (10 words each)
+constexpr int kLaneGranules = kTabAGranules + kParkGranules + kPrefGranules;
 constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
 
 // Per-lane table [0..8](-A) in global scratch. Layout: lane-contiguous, 9 entries x 160 B per lane
@@ -96,10 +107,10 @@ struct LdsTabB {
   }
 };
 
-// Fixed-base table [0..2^15]B (affine Niels, 8 x 16 B per entry, 4.2 MB) in global memory: L2/MALL
-// resident, read through an LDS-DMA prefetch like the A entries.
-constexpr int kBtab16Entries = (1 << 15) + 1;
-struct DevTabB16 {
+// Fixed-base table [0..2^(kBWin-1)]B (affine Niels, 8 x 16 B per entry: 4.2 MB for 16-bit windows,
+// 67 MB for 20, 1.07 GB for 24) in global memory, read through an LDS-DMA prefetch like the A entries.
+constexpr int kBtabEntries = (1 << (kBWin - 1)) + 1;
+struct DevTabB {
   const int4* base;
   int4* stage;  // this wave's 8 x 1 KiB LDS staging buffer
   int lane;
@@ -151,10 +162,26 @@ __device__ AT2V_INLINE uint32_t load_u32_guarded(const uint8_t* buf, uint32_t a,
   return v;
 }
 
+// store / load a group-local field element or p2 point in this lane's scratch slot (lane-contiguous)
+__device__ AT2V_INLINE void slot_store(int4* dst, const int32_t* w, int nw) {
+  for (int q = 0; q < (nw + 3) / 4; ++q)
+    dst[q] = make_int4(w[4 * q], 4 * q + 1 < nw ? w[4 * q + 1] : 0, 4 * q + 2 < nw ? w[4 * q + 2] : 0,
+                       4 * q + 3 < nw ? w[4 * q + 3] : 0);
+}
+__device__ AT2V_INLINE void slot_load(int32_t* w, const int4* src, int nw) {
+  for (int q = 0; q < (nw + 3) / 4; ++q) {
+    const int4 v = src[q];
+    w[4 * q] = v.x;
+    if (4 * q + 1 < nw) w[4 * q + 1] = v.y;
+    if (4 * q + 2 < nw) w[4 * q + 2] = v.z;
+    if (4 * q + 3 < nw) w[4 * q + 3] = v.w;
+  }
+}
+
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab16) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 bstage[kWavesPerBlock * 8 * 64];
   const int lane = threadIdx.x & 63;
@@ -164,19 +191,18 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   const uint32_t nwords = (n + 31) / 32;
   int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
   DevTabA ta{slot, astage + (threadIdx.x >> 6) * 640, lane};
-  DevTabB16 tb{btab16, bstage + (threadIdx.x >> 6) * 512, lane};
-  int4* park = slot + kTabAGranules;
-  // Chunks are taken in pairs (c, c + nwaves): one field inversion serves both (Montgomery's trick).
-  // The ladder body appears once (rolled loop over the pair); R'_1 is parked in scratch meanwhile.
-  for (uint32_t c = wave; c < nchunks; c += 2 * nwaves) {
-    const uint32_t c2 = c + nwaves;
-    const int npair = c2 < nchunks ? 2 : 1;
-    int ok0 = 0, ok1 = 0;
-    ge_p2 Rp;
+  DevTabB tb{btab, bstage + (threadIdx.x >> 6) * 512, lane};
+  int4* park = slot + kTabAGranules;                 // kGroup x 8 granules: R' of chunk h of the group
+  int4* pref = slot + kTabAGranules + kParkGranules;  // (kGroup-1) x 3 granules: Z_0 * .. * Z_h
+  // Chunks are taken in groups (c, c + nwaves, ..., c + (kGroup-1) nwaves): one field inversion serves the
+  // whole group (Montgomery's trick, 3 M per extra chunk). The ladder body appears once (rolled loop).
+  for (uint32_t c = wave; c < nchunks; c += kGroup * nwaves) {
+    const int cnt = (int)min((uint32_t)kGroup, (nchunks - c + nwaves - 1) / nwaves);
+    uint32_t okbits = 0;
     AT2V_PHASE(0);
 #pragma unroll 1
-    for (int h = 0; h < npair; ++h) {
-      const uint32_t chunk = h ? c2 : c;
+    for (int h = 0; h < cnt; ++h) {
+      const uint32_t chunk = c + (uint32_t)h * nwaves;
       const uint32_t i = chunk * 64 + lane;
       const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
       uint32_t Rw[8], Sw[8], Aw[8];
@@ -193,46 +219,44 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
         const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
         return __builtin_amdgcn_alignbit(hi, lo, sh);
       };
-      const int ok = verify_ladder(Rp, Rw, Aw, Sw, len, msgword, policy, ta, tb) & (i < n);
-      ok0 = h ? ok0 : ok;
-      ok1 = h ? ok : ok1;
-      if (h == 0 && npair == 2) {  // park R'_1 in this lane's scratch slot while the second chunk runs
-        const int32_t* w = reinterpret_cast<const int32_t*>(&Rp);
-#pragma unroll
-        for (int q = 0; q < 7; ++q) park[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-        park[7] = make_int4(w[28], w[29], 0, 0);
-      }
+      ge_p2 Rp;
+      const int ok = verify_ladder<kBWin>(Rp, Rw, Aw, Sw, len, msgword, policy, ta, tb) & (i < n);
+      okbits |= (uint32_t)ok << h;
+      slot_store(park + 8 * h, reinterpret_cast<const int32_t*>(&Rp), 30);
     }
-    ge_p2 R1;  // first chunk's R'
-    fe zi1, zi2;
-    if (npair == 2) {
-      int32_t* w = reinterpret_cast<int32_t*>(&R1);
-#pragma unroll
-      for (int q = 0; q < 7; ++q) {
-        const int4 v = park[q];
-        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-      }
-      const int4 v = park[7];
-      w[28] = v.x;
-      w[29] = v.y;
-      fe z12, inv;
-      fe_mul(z12, R1.Z, Rp.Z);
-      fe_invert(inv, z12);
-      fe_mul(zi1, inv, Rp.Z);
-      fe_mul(zi2, inv, R1.Z);
-    } else {
-      R1 = Rp;
-      fe_invert(zi1, Rp.Z);
-    }
-    AT2V_PHASE(5);
+    // prefix products P_h = Z_0 ... Z_h (P_0..P_{cnt-2} kept in scratch), one inversion of P_{cnt-1}
+    fe acc;
+    slot_load(acc.v, park + 5, 10);  // Z of chunk 0 (words 20..29 of the parked point)
 #pragma unroll 1
-    for (int h = 0; h < npair; ++h) {
-      const uint32_t chunk = h ? c2 : c;
+    for (int h = 1; h < cnt; ++h) {
+      slot_store(pref + 3 * (h - 1), acc.v, 10);
+      fe z;
+      slot_load(z.v, park + 8 * h + 5, 10);
+      fe_mul(acc, acc, z);
+    }
+    fe inv;
+    fe_invert(inv, acc);
+    AT2V_PHASE(5);
+    // backwards: 1/Z_h = inv_h * P_{h-1} with inv_h = 1/P_h; inv_{h-1} = inv_h * Z_h
+#pragma unroll 1
+    for (int h = cnt - 1; h >= 0; --h) {
+      ge_p2 R;
+      slot_load(reinterpret_cast<int32_t*>(&R), park + 8 * h, 30);
+      fe zi;
+      if (h > 0) {
+        fe p;
+        slot_load(p.v, pref + 3 * (h - 1), 10);
+        fe_mul(zi, inv, p);
+        fe_mul(inv, inv, R.Z);
+      } else {
+        zi = inv;
+      }
+      const uint32_t chunk = c + (uint32_t)h * nwaves;
       const uint32_t i = chunk * 64 + lane;
       const uint32_t ii = i < n ? i : n - 1;
       uint32_t Rr[8];
       load8(Rr, sig + (size_t)ii * 64);
-      const int good = (h ? ok1 : ok0) & verify_finish(h ? Rp : R1, h ? zi2 : zi1, Rr);
+      const int good = (int)((okbits >> h) & 1u) & verify_finish(R, zi, Rr);
       const uint64_t mask = __ballot(good);
       if (lane == 0) {
         verdicts[2 * chunk] = (uint32_t)mask;
@@ -427,13 +451,13 @@ __global__ __launch_bounds__(kBlock) void sign_kernel(const uint8_t* __restrict_
   for (int q = 0; q < 16; ++q) sgo[q] = sigw[q];
 }
 
-// [j]B, j = 0..2^15, affine Niels, 32 words per entry (30 + 2 pad): built once per context
-__global__ __launch_bounds__(kBlock) void build_btab16_kernel(int4* __restrict__ out) {
+// [j]B, j = 0..2^(kBWin-1), affine Niels, 32 words per entry (30 + 2 pad): built once per context
+__global__ __launch_bounds__(kBlock) void build_btab_kernel(int4* __restrict__ out) {
   __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
   stage_btab(btab);
   LdsTabB tb{btab};
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= (uint32_t)kBtab16Entries) return;
+  if (j >= (uint32_t)kBtabEntries) return;
   uint32_t sj[8] = {j, 0, 0, 0, 0, 0, 0, 0};
   ge_p2 P;
   ge_scalarmult_base(P, sj, tb);
@@ -473,22 +497,22 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
 
 // ------------------------------------------------------------------ launchers (host side)
 
-size_t btab16_bytes() { return (size_t)kBtab16Entries * 8 * 16; }
+size_t btab_bytes() { return (size_t)kBtabEntries * 8 * 16; }
 
-hipError_t launch_build_btab16(int4* out, hipStream_t stream) {
-  hipLaunchKernelGGL(build_btab16_kernel, dim3((kBtab16Entries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out);
+hipError_t launch_build_btab(int4* out, hipStream_t stream) {
+  hipLaunchKernelGGL(build_btab_kernel, dim3((kBtabEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out);
   return hipGetLastError();
 }
 
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab16, int grid, hipStream_t stream) {
+                         const int4* btab, int grid, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t need_blocks = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
   hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                     verdicts, scratch, btab16);
+                     verdicts, scratch, btab);
   return hipGetLastError();
 }
 

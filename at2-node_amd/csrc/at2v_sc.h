@@ -144,4 +144,27 @@ AT2V_HD AT2V_INLINE void sc_recode16(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-2^WB digits e_0..e_{ND-1} of a scalar < 2^253 (WB in {16, 20, 24}, ND = ceil(254 / WB)),
+// e_j in [-2^(WB-1), 2^(WB-1)), stored one per word as e_j + 2^(WB-1).
+template <int WB>
+struct ScWin {
+  static constexpr int ND = (254 + WB - 1) / WB;
+};
+template <int WB>
+AT2V_HD AT2V_INLINE void sc_recode_w(uint32_t out[ScWin<WB>::ND], const uint32_t s[8]) {
+  constexpr int ND = ScWin<WB>::ND;
+  int carry = 0;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const int bit = WB * j, k = bit >> 5, sh = bit & 31;
+    uint32_t raw = k < 8 ? (s[k] >> sh) : 0u;
+    if (sh && k + 1 < 8) raw |= s[k + 1] << (32 - sh);
+    raw &= (1u << WB) - 1u;
+    int d = (int)raw + carry;
+    carry = (d + (1 << (WB - 1))) >> WB;
+    d -= carry << WB;
+    out[j] = (uint32_t)(d + (1 << (WB - 1)));
+  }
+}
+
 }  // namespace at2v

@@ -7,9 +7,10 @@
 // Double-scalar multiplication R' = [k](-A) + [s]B uses one shared doubling chain with
 // wavefront-uniform fixed windows (every lane adds at the same positions, no divergence):
 //   k : 64 signed radix-16 digits  in [-8, 8]     -> table [0..8](-A), cached form, per lane (global scratch)
-//   s : 16 signed radix-2^16 digits in [-2^15, 2^15] -> table [0..2^15]B, affine Niels, 4.2 MB in global
-//       memory (L2/MALL), entries prefetched into LDS by LDS-DMA
-//   R = sum_i 16^i (k_i(-A) + [4 | i] s_{i/4} B), Horner from i = 63: 252 doublings, 64 + 16 additions.
+//   s : ceil(254/WB) signed radix-2^WB digits (WB = 16, 20 or 24) -> table [0..2^(WB-1)]B, affine Niels,
+//       in global memory (L2/MALL), entries prefetched into LDS by LDS-DMA
+//   R = sum_i 16^i (k_i(-A) + [WB/4 | i] s_{4i/WB} B), Horner from i = 63: 252 doublings, 64 + ceil(254/WB)
+//   additions.
 // Any correct evaluation of [k](-A) + [s]B yields the same group element, so verdicts are
 // identical to dalek's NAF-5/NAF-8 vartime ladder (the oracle restates that one).
 #pragma once
@@ -27,13 +28,15 @@ namespace at2v {
 
 enum { POLICY_DALEK_V1 = 0, POLICY_LIBSODIUM_1_0_18 = 1 };
 
-// uniform-index select from an 8-word register array (avoids scratch for a runtime index)
-AT2V_HD AT2V_INLINE uint32_t sel8(const uint32_t w[8], int j) {
+// uniform-index select from an N-word register array (avoids scratch for a runtime index)
+template <int N>
+AT2V_HD AT2V_INLINE uint32_t seln(const uint32_t* w, int j) {
   uint32_t r = w[0];
 #pragma unroll
-  for (int m = 1; m < 8; ++m) r = (j == m) ? w[m] : r;
+  for (int m = 1; m < N; ++m) r = (j == m) ? w[m] : r;
   return r;
 }
+AT2V_HD AT2V_INLINE uint32_t sel8(const uint32_t w[8], int j) { return seln<8>(w, j); }
 
 // y-encoding (sign bit ignored) is canonical, i.e. y < p (libsodium ge25519_is_canonical)
 AT2V_HD AT2V_INLINE int enc_y_canonical(const uint32_t s[8]) {
@@ -87,9 +90,11 @@ AT2V_HD AT2V_INLINE void ge_scalarmult_base(ge_p2& out, const uint32_t s[8], con
 // Table access policies.
 //   TabA: void store(int e, const ge_cached&); void load(int e, ge_cached&);  (per lane, e in 0..8)
 //         void prefetch(int e); void load_prefetched(ge_cached&)   (asynchronous load of one entry)
-//   TabB: void prefetch(int e); void load_prefetched(ge_niels&)               (shared, e in 0..32768)
+//   TabB: void prefetch(int e); void load_prefetched(ge_niels&)               (shared, e in 0..2^(WB-1))
+// WB = bits per fixed-base window (16, 20 or 24): s gets ceil(254/WB) signed digits, one every WB/4
+// radix-16 windows, against a table [0..2^(WB-1)]B.
 // V1..V4: checks, decode, hash, ladder. Returns the checks' verdict; R' = [k](-A) + [s]B in Rp.
-template <class TabA, class TabB, class MsgWord>
+template <int WB, class TabA, class TabB, class MsgWord>
 AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
                                       uint32_t len, MsgWord msgword, int policy, TabA& ta, const TabB& tb) {
   // V1: s < l
@@ -117,9 +122,11 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
     sha512_digest_words(hw, h);
     sc_reduce512(k, hw);
   }
-  uint32_t kd[8], sd[8];
+  constexpr int ND = ScWin<WB>::ND, WW = WB / 4;  // s digits; radix-16 windows per s digit
+  static_assert(WB % 4 == 0 && (ND - 1) * WW <= 62, "s digits must sit on radix-16 windows below the top");
+  uint32_t kd[8], sd[ND];
   sc_recode4(kd, k);
-  sc_recode16(sd, Sw);
+  sc_recode_w<WB>(sd, Sw);
   AT2V_PHASE(2);
 
   // table [j](-A), j = 0..8
@@ -160,8 +167,9 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
     const int d = (int)((sel8(kd, i >> 3) >> (4 * (i & 7))) & 15) - 8;
     ta.prefetch(d < 0 ? -d : d);  // both tables land while the window's four doublings run
     int e = 0;
-    if ((i & 3) == 0) {  // s digit j = i/4 (radix 2^16) at every fourth radix-16 window
-      e = (int)((sel8(sd, i >> 3) >> (16 * ((i >> 2) & 1))) & 0xffff) - 0x8000;
+    const bool bwin = (i % WW) == 0 && i / WW < ND;  // s digit j = i / WW (radix 2^WB)
+    if (bwin) {
+      e = (int)seln<ND>(sd, i / WW) - (1 << (WB - 1));
       tb.prefetch(e < 0 ? -e : e);
     }
     for (int r = 0; r < 3; ++r) {
@@ -173,7 +181,7 @@ AT2V_HD AT2V_INLINE int verify_ladder(ge_p2& Rp, const uint32_t Rw[8], const uin
     ge_p1p1_to_p3(R3, t);
     ge_cached_cneg(ca, d < 0);
     ge_add(t, R3, ca);
-    if ((i & 3) == 0) {
+    if (bwin) {
       ge_p1p1_to_p3(R3, t);
       tb.load_prefetched(nb);
       ge_niels_cneg(nb, e < 0);
@@ -202,11 +210,11 @@ AT2V_HD AT2V_INLINE int verify_finish(const ge_p2& Rp, const fe& zinv, const uin
   return eq;
 }
 
-template <class TabA, class TabB, class MsgWord, class RLoad>
+template <int WB, class TabA, class TabB, class MsgWord, class RLoad>
 AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                     MsgWord msgword, int policy, TabA& ta, const TabB& tb, RLoad rload) {
   ge_p2 Rp;
-  const int ok = verify_ladder(Rp, Rw, Aw, Sw, len, msgword, policy, ta, tb);
+  const int ok = verify_ladder<WB>(Rp, Rw, Aw, Sw, len, msgword, policy, ta, tb);
   fe zinv;
   fe_invert(zinv, Rp.Z);
   uint32_t Rr[8];

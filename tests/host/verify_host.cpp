@@ -84,8 +84,8 @@ int main(int argc, char** argv) {
     static HostTabB16 tb;
     HostTabA ta;
     auto rl = [&](uint32_t r[8]) { for (int q = 0; q < 8; ++q) r[q] = R[q]; };
-    int d = verify_core(R, A, S, len, mw, POLICY_DALEK_V1, ta, tb, rl);
-    int s = verify_core(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tb, rl);
+    int d = verify_core<16>(R, A, S, len, mw, POLICY_DALEK_V1, ta, tb, rl);
+    int s = verify_core<16>(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tb, rl);
     if (d != vd[i]) { if (bad_d < 10) fprintf(stderr, "dalek mismatch i=%zu cls=%d got=%d want=%d\n", i, cls[i], d, vd[i]); ++bad_d; }
     if (s != vs[i]) { if (bad_s < 10) fprintf(stderr, "sodium mismatch i=%zu cls=%d got=%d want=%d\n", i, cls[i], s, vs[i]); ++bad_s; }
   }

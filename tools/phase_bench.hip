@@ -55,8 +55,8 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&off, (size_t)(n + 1) * 4));
   CHECK(hipMalloc(&ver, (size_t)(n + 31) / 32 * 4));
   CHECK(hipMalloc(&scratch, (size_t)grid * at2v::scratch_bytes_per_block()));
-  CHECK(hipMalloc(&btab, at2v::btab16_bytes()));
-  CHECK(at2v::launch_build_btab16(btab, 0));
+  CHECK(hipMalloc(&btab, at2v::btab_bytes()));
+  CHECK(at2v::launch_build_btab(btab, 0));
   CHECK(at2v::launch_gen(0x4154325F, 0, n, L, pk, sig, msg, off, 0));
   CHECK(hipDeviceSynchronize());
   std::vector<unsigned long long> zero(AT2V_MAX_WAVES * 8, 0), zl(AT2V_MAX_WAVES, 0);
@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
   size_t valid = 0;
   for (uint32_t i = 0; i < n; ++i) valid += (hv[i / 32] >> (i % 32)) & 1;
   const char* names[8] = {"pair/loop overhead", "loads+V1+decompress", "sha512+mod l+recode", "A table",
-                          "ladder", "pair inversion", "encode+compare+store", "-"};
+                          "ladder", "group inversion", "encode+compare+store", "-"};
   double tot = 0, b[8] = {0};
   const int waves = grid * 4;
   for (int w = 0; w < waves; ++w)
