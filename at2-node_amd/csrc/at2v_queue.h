@@ -21,6 +21,7 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace at2v {
@@ -49,7 +50,7 @@ struct QueueSlot {
   size_t n = 0, msg_used = 0;
   uint64_t first_ticket = 0;
   uint64_t t_first = 0;
-  std::vector<uint64_t> t_submit;
+  std::vector<std::pair<uint32_t, uint64_t>> t_runs;  // (records, submit time) per submit call
   int status = 0;
   void* backend = nullptr;
 };
@@ -73,7 +74,6 @@ class BatchQueue {
       s.cap_msg = std::max<size_t>(o_.max_batch * o_.max_msg_bytes, 64);
       const int e = be_.alloc(s);
       if (e) return e;
-      s.t_submit.reserve(o_.max_batch);
       free_.push_back(&s);
     }
     running_ = true;
@@ -110,9 +110,11 @@ class BatchQueue {
     for (size_t i = 0; i < n; ++i)  // validate the whole call before taking any record
       if (off[i + 1] < off[i] || off[i + 1] - off[i] > slots_[0].cap_msg) return -1;
     if (first_ticket) *first_ticket = next_ticket_;
-    for (size_t i = 0; i < n; ++i) {
-      const uint32_t len = off[i + 1] - off[i];
-      if (fill_ && (fill_->n == fill_->cap_records || fill_->msg_used + len > fill_->cap_msg)) seal_locked();
+    const uint64_t t = now_us();  // one submit time for the whole call
+    size_t i = 0;
+    while (i < n) {
+      if (fill_ && (fill_->n == fill_->cap_records || fill_->msg_used + (off[i + 1] - off[i]) > fill_->cap_msg))
+        seal_locked();
       if (!fill_) {
         cv_free_.wait(lk, [&] { return fill_ || !free_.empty() || !running_; });
         if (!running_) return -1;
@@ -123,24 +125,37 @@ class BatchQueue {
         fill_->n = 0;
         fill_->msg_used = 0;
         fill_->first_ticket = next_ticket_;
-        fill_->t_submit.clear();
+        fill_->t_runs.clear();
         fill_->off[0] = 0;
       }
       QueueSlot& s = *fill_;
-      const uint64_t t = now_us();
       if (s.n == 0) {
         s.t_first = t;
         cv_launch_.notify_all();  // arm the deadline
       }
-      std::memcpy(s.pk + 32 * s.n, pk + 32 * i, 32);
-      std::memcpy(s.sig + 64 * s.n, sig + 64 * i, 64);
-      if (len) std::memcpy(s.msg + s.msg_used, msg + off[i], len);
-      s.msg_used += len;
-      s.t_submit.push_back(t);
-      ++s.n;
-      s.off[s.n] = (uint32_t)s.msg_used;
-      ++next_ticket_;
-      ++stats_.submitted;
+      // bulk-copy the longest run of records that fits the slot (records and message bytes)
+      size_t m = std::min(n - i, s.cap_records - s.n);
+      const size_t room = s.cap_msg - s.msg_used;
+      if (off[i + m] - off[i] > room) {  // offsets are non-decreasing: binary search the message-byte limit
+        size_t lo = 1, hi = m;             // off[i+1]-off[i] <= room holds (checked above)
+        while (lo < hi) {
+          const size_t mid = (lo + hi + 1) / 2;
+          if (off[i + mid] - off[i] <= room) lo = mid; else hi = mid - 1;
+        }
+        m = lo;
+      }
+      const uint32_t mb = off[i + m] - off[i];
+      std::memcpy(s.pk + 32 * s.n, pk + 32 * i, 32 * m);
+      std::memcpy(s.sig + 64 * s.n, sig + 64 * i, 64 * m);
+      if (mb) std::memcpy(s.msg + s.msg_used, msg + off[i], mb);
+      const uint32_t base = (uint32_t)s.msg_used - off[i];
+      for (size_t k = 1; k <= m; ++k) s.off[s.n + k] = off[i + k] + base;
+      s.msg_used += mb;
+      s.n += m;
+      s.t_runs.emplace_back((uint32_t)m, t);
+      next_ticket_ += m;
+      stats_.submitted += m;
+      i += m;
       if (s.n == s.cap_records) seal_locked();
     }
     return 0;
@@ -255,8 +270,10 @@ class BatchQueue {
       Done d{s->first_ticket, s->n, 0, st != 0, {}};
       d.words.assign(s->verdicts, s->verdicts + (s->n + 31) / 32);
       done_.push_back(std::move(d));
-      for (uint64_t ts : s->t_submit) {
-        if (lat_.size() < kMaxLatencySamples) lat_.push_back((uint32_t)std::min<uint64_t>(t - ts, UINT32_MAX));
+      for (const auto& r : s->t_runs) {
+        const uint32_t d = (uint32_t)std::min<uint64_t>(t - r.second, UINT32_MAX);
+        const size_t k = std::min<size_t>(r.first, kMaxLatencySamples - std::min(kMaxLatencySamples, lat_.size()));
+        lat_.insert(lat_.end(), k, d);
       }
       stats_.completed += s->n;
       ++stats_.batches;

@@ -176,7 +176,7 @@ def main():
                 "hbm_frac": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9 / HBM_PEAK_GBS,
             },
         }
-    if rank == 0 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args, d_pk, d_sig, d_msg, n, L)
     if rank == 0 and world == 1 and args.pmc_traffic:
         tr = pmc_traffic(args, n, L)
