@@ -20,8 +20,14 @@ namespace at2v {
 #define AT2V_VERIFY_WAVES_PER_SIMD 2  // register budget: 512 / waves VGPR+AGPR per lane
 #endif
 
+#ifndef AT2V_VERIFY_HALF
+#define AT2V_VERIFY_HALF 1  // 1: half-size equation; 0: full-length ladder (§4)
+#endif
 #ifndef AT2V_BWIN
 #define AT2V_BWIN 16  // fixed-base window bits: table [0..2^(AT2V_BWIN-1)]B
+#endif
+#if AT2V_VERIFY_HALF && AT2V_BWIN != 16
+#error "the half-size path uses 16-bit fixed-base windows"
 #endif
 #ifndef AT2V_INV_GROUP
 #define AT2V_INV_GROUP 2  // chunks whose final inversions share one field inversion (Montgomery's trick)
@@ -33,9 +39,15 @@ constexpr int kBWin = AT2V_BWIN;
 constexpr int kGroup = AT2V_INV_GROUP;
 static_assert(kGroup >= 1 && kGroup <= 8, "inversion group");
 constexpr int kTabAGranules = 9 * 10;            // 9 entries x 10 x 16 B
+#if AT2V_VERIFY_HALF
+constexpr int kLaneGranules = 2 * kTabAGranules;  // tables [j]A and [j](+-R)
+constexpr int kNumBtabs = 2;                      // [j]B and [j 2^128]B
+#else
 constexpr int kParkGranules = 8 * kGroup;        // parked R' (X, Y, Z: 30 words) of every chunk of a group
 constexpr int kPrefGranules = 3 * (kGroup - 1);  // prefix products Z_0..Z_h of the group (10 words each)
 constexpr int kLaneGranules = kTabAGranules + kParkGranules + kPrefGranules;
+constexpr int kNumBtabs = 1;
+#endif
 constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
 
 // Per-lane table [0..8](-A) in global scratch. Layout: lane-contiguous, 9 entries x 160 B per lane
@@ -115,6 +127,7 @@ struct DevTabB {
   int4* stage;  // this wave's 8 x 1 KiB LDS staging buffer
   int lane;
   __device__ AT2V_INLINE void prefetch(int e) const {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage may be shared with a just-read entry
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + e * 8 + q),
@@ -178,6 +191,63 @@ __device__ AT2V_INLINE void slot_load(int32_t* w, const int4* src, int nw) {
   }
 }
 
+#if AT2V_VERIFY_HALF
+__device__ AT2V_INLINE int wave_max_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Half-size verification: one chunk of 64 records per wave, no final inversion.
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t nchunks = (n + 63) / 64;
+  const uint32_t nwords = (n + 31) / 32;
+  int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
+  DevTabA ta{slot, astage + wib * 640, lane};
+  DevTabA tr{slot + kTabAGranules, rstage + wib * 640, lane};
+  const DevTabB tb0{btab, astage + wib * 640, lane};                      // [j]B, staged where A's entry was
+  const DevTabB tb1{btab + (size_t)kBtabEntries * 8, rstage + wib * 640, lane};  // [j 2^128]B, in R's stage
+  auto wmax = [](int v) { return wave_max_i32(v); };
+  for (uint32_t c = wave; c < nchunks; c += nwaves) {
+    AT2V_PHASE(0);
+    const uint32_t i = c * 64 + lane;
+    const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
+    uint32_t Rw[8], Sw[8], Aw[8];
+    load8(Rw, sig + (size_t)ii * 64);
+    load8(Sw, sig + (size_t)ii * 64 + 32);
+    load8(Aw, pk + (size_t)ii * 32);
+    const uint32_t o0 = off[ii];
+    const uint32_t len = off[ii + 1] - o0;
+    auto msgword = [&](uint32_t j) -> uint32_t {
+      const uint32_t a = o0 + 4 * j;
+      const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+      const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+      if (sh == 0) return lo;
+      const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+      return __builtin_amdgcn_alignbit(hi, lo, sh);
+    };
+    const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax) & (i < n);
+    const uint64_t mask = __ballot(good);
+    if (lane == 0) {
+      verdicts[2 * c] = (uint32_t)mask;
+      if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
+    }
+    AT2V_PHASE(6);
+  }
+}
+#else
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
@@ -266,6 +336,8 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     AT2V_PHASE(6);
   }
 }
+
+#endif  // AT2V_VERIFY_HALF
 
 // ------------------------------------------------------------------ signing side
 
@@ -452,13 +524,15 @@ __global__ __launch_bounds__(kBlock) void sign_kernel(const uint8_t* __restrict_
 }
 
 // [j]B, j = 0..2^(kBWin-1), affine Niels, 32 words per entry (30 + 2 pad): built once per context
-__global__ __launch_bounds__(kBlock) void build_btab_kernel(int4* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void build_btab_kernel(int4* __restrict__ out, int shift_words) {
   __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
   stage_btab(btab);
   LdsTabB tb{btab};
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= (uint32_t)kBtabEntries) return;
-  uint32_t sj[8] = {j, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t sj[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) sj[q] = q == shift_words ? j : 0u;  // j * 2^(32 shift_words)
   ge_p2 P;
   ge_scalarmult_base(P, sj, tb);
   ge_niels nj;
@@ -497,11 +571,17 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
 
 // ------------------------------------------------------------------ launchers (host side)
 
-size_t btab_bytes() { return (size_t)kBtabEntries * 8 * 16; }
+size_t btab_bytes() { return (size_t)kNumBtabs * kBtabEntries * 8 * 16; }
 
+// table t (t = 0: [j]B; t = 1: [j 2^128]B for the half-size path) at out + t * kBtabEntries * 8
 hipError_t launch_build_btab(int4* out, hipStream_t stream) {
-  hipLaunchKernelGGL(build_btab_kernel, dim3((kBtabEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out);
-  return hipGetLastError();
+  for (int t = 0; t < kNumBtabs; ++t) {
+    hipLaunchKernelGGL(build_btab_kernel, dim3((kBtabEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                       out + (size_t)t * kBtabEntries * 8, 4 * t);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,

@@ -108,6 +108,25 @@ AT2V_HD AT2V_INLINE void sc_recode4(uint32_t out[8], const uint32_t s[8]) {
   // carry out of digit 63 is 0 for s < 2^253 (digit 63 <= 1 + 1)
 }
 
+// Signed radix-16 digits d_i in [-7, 8] (stored as d_i + 7 nibbles): a value < 2^(4m-1) needs only m digits
+// (its top nibble <= 7 plus a carry is at most 8, so nothing carries out). Used for the half-size
+// scalars, whose window count is the wave maximum of that m.
+AT2V_HD AT2V_INLINE void sc_recode4_hi8(uint32_t out[8], const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      int d = (int)((s[j] >> (4 * m)) & 15) + carry;
+      carry = (d + 7) >> 4;
+      d -= carry << 4;
+      w |= (uint32_t)(d + 7) << (4 * m);
+    }
+    out[j] = w;
+  }
+}
+
 // Signed radix-256 digits e_0..e_31 of a scalar < 2^253, e_i in [-128, 127], stored as (e_i + 128)
 // bytes: word j holds digits 4j..4j+3.
 AT2V_HD AT2V_INLINE void sc_recode8(uint32_t out[8], const uint32_t s[8]) {

@@ -15,6 +15,7 @@
 // identical to dalek's NAF-5/NAF-8 vartime ladder (the oracle restates that one).
 #pragma once
 #include "at2v_ge.h"
+#include "at2v_lattice.h"
 #include "at2v_sc.h"
 #include "at2v_sha512.h"
 
@@ -220,6 +221,157 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
   uint32_t Rr[8];
   rload(Rr);
   return ok & verify_finish(Rp, zinv, Rr);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Half-size verification (tools/halfscalar_proto.py). Same verdicts as verify_core:
+//   accept  <=>  s < l, A decodes, R_bytes canonical and decodes, and V = [c1]R + [c0]A - [t]B = 0,
+// with (c0, c1) from lattice_reduce(k) (c0 = c1 k mod 8l, c1 odd) and t = c1 s mod l. V = [c1](R - R')
+// for R' = [s]B - [k]A exactly (every point has [8l]P = 0), and [c1] is injective on E (c1 odd, 0 < |c1|
+// < l), so V = 0 <=> R = R' <=> (R_bytes canonical) enc(R') == R_bytes. The doubling chain covers only
+// max(|c0|, |c1|) ~ 2^128 (wave maximum, >= 29 windows): ~128 doublings instead of 252, two variable-base
+// tables (A, +-R) and two fixed-base tables [j]B, [j 2^128]B (16-bit windows, t split at bit 128).
+//   TabP : store(e, cached) / prefetch(e) / load_prefetched(cached)   (per lane, e in 0..8)
+//   TabB : prefetch(e) / load_prefetched(niels)                       (shared, e in 0..2^15)
+//   WaveMax : int(int) -> maximum over the lanes that verify together (identity on the host)
+template <class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax>
+AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                    MsgWord msgword, int policy, TabP& ta, TabP& tr, const TabB0& tb0,
+                                    const TabB1& tb1, WaveMax wave_max) {
+  // V1: s < l
+  int ok = sc_is_canonical(Sw);
+  if (policy == POLICY_LIBSODIUM_1_0_18) {
+    ok &= !enc_small_order(Rw);
+    ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
+  }
+  // V2: decode A; R must be canonical (y < p, not x = 0 with the sign bit) and decode
+  ge_p3 A, R;
+  ok &= ge_frombytes(A, Aw);
+  ok &= enc_y_canonical(Rw);
+  ok &= ge_frombytes(R, Rw);
+  ok &= !(fe_iszero(R.X) & (int)(Rw[7] >> 31));
+  AT2V_PHASE(1);
+  // V3: k = SHA-512(R || A || M) mod l
+  uint32_t k[8];
+  {
+    uint32_t pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = Rw[i];
+      pre[8 + i] = Aw[i];
+    }
+    uint64_t h[8];
+    sha512_prefixed<16>(h, pre, len, msgword);
+    uint32_t hw[16];
+    sha512_digest_words(hw, h);
+    sc_reduce512(k, hw);
+  }
+  AT2V_PHASE(5);
+  // half-size scalars
+  HalfScalars hs;
+  lattice_reduce(hs, k);
+  AT2V_PHASE(7);
+  uint32_t t[8];
+  sc_mul_signed(t, hs, Sw);
+  uint32_t c0d[8], c1d[8], td[8];
+  sc_recode4_hi8(c0d, hs.c0);
+  sc_recode4_hi8(c1d, hs.c1);
+  sc_recode16(td, t);
+  const int nw_lane = ok ? hs.bits / 4 + 1 : 0;  // windows for values < 2^(4 nw - 1)
+  int nw = wave_max(nw_lane);
+  nw = nw < 29 ? 29 : nw;  // B digits sit at windows 0, 4, ..., 28
+  AT2V_PHASE(2);
+
+  // tables [j]A and [j](+-R), j = 0..8
+  if (hs.c1_neg) {
+    fe_neg(R.X, R.X);
+    fe_neg(R.T, R.T);
+  }
+#pragma unroll 1
+  for (int side = 0; side < 2; ++side) {
+    const ge_p3& P0 = side ? R : A;
+    TabP& tp = side ? tr : ta;
+    ge_cached c1, cj;
+    ge_cached_identity(cj);
+    tp.store(0, cj);
+    ge_p3_to_cached(c1, P0);
+    tp.store(1, c1);
+    ge_p3 P = P0;
+    for (int j = 2; j <= 8; ++j) {
+      ge_p1p1 tt;
+      ge_add(tt, P, c1);
+      ge_p1p1_to_p3(P, tt);
+      ge_p3_to_cached(cj, P);
+      tp.store(j, cj);
+    }
+  }
+  AT2V_PHASE(3);
+
+  // shared doubling chain over windows nw-1 .. 0:
+  //   acc = 16 acc + a_i A + r_i (+-R) + [4 | i, i < 32] (-t_{i/4} [2^(16 i/4)]B - t_{8+i/4} [2^(128+16 i/4)]B)
+  ge_p2 R2;
+  ge_p3 R3;
+  ge_p1p1 tt;
+  ge_cached ca;
+  ge_niels nb;
+  auto digit4 = [](const uint32_t d[8], int i) -> int { return (int)((sel8(d, i >> 3) >> (4 * (i & 7))) & 15) - 7; };
+  {
+    const int i = nw - 1;
+    const int da = digit4(c0d, i), dr = digit4(c1d, i);
+    ta.prefetch(da < 0 ? -da : da);
+    tr.prefetch(dr < 0 ? -dr : dr);
+    ge_p3_identity(R3);
+    ta.load_prefetched(ca);
+    ge_cached_cneg(ca, da < 0);
+    ge_add(tt, R3, ca);
+    ge_p1p1_to_p3(R3, tt);
+    tr.load_prefetched(ca);
+    ge_cached_cneg(ca, dr < 0);
+    ge_add(tt, R3, ca);
+    ge_p1p1_to_p2(R2, tt);
+  }
+  for (int i = nw - 2; i >= 0; --i) {
+    const int da = digit4(c0d, i), dr = digit4(c1d, i);
+    ta.prefetch(da < 0 ? -da : da);  // both land while the window's four doublings run
+    tr.prefetch(dr < 0 ? -dr : dr);
+    for (int r = 0; r < 3; ++r) {
+      ge_p2_dbl(tt, R2);
+      ge_p1p1_to_p2(R2, tt);
+    }
+    ge_p2_dbl(tt, R2);
+    ge_p1p1_to_p3(R3, tt);
+    const bool bwin = (i & 3) == 0 && i < 32;
+    int e0 = 0, e1 = 0;
+    if (bwin) {  // -t digits j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B)
+      e0 = (1 << 15) - (int)((sel8(td, i >> 3) >> (16 * ((i >> 2) & 1))) & 0xffff);
+      e1 = (1 << 15) - (int)((sel8(td, 4 + (i >> 3)) >> (16 * ((i >> 2) & 1))) & 0xffff);
+    }
+    ta.load_prefetched(ca);
+    if (bwin) tb0.prefetch(e0 < 0 ? -e0 : e0);  // into A's stage, now consumed
+    ge_cached_cneg(ca, da < 0);
+    ge_add(tt, R3, ca);
+    ge_p1p1_to_p3(R3, tt);
+    tr.load_prefetched(ca);
+    if (bwin) tb1.prefetch(e1 < 0 ? -e1 : e1);  // into R's stage
+    ge_cached_cneg(ca, dr < 0);
+    ge_add(tt, R3, ca);
+    if (bwin) {
+      ge_p1p1_to_p3(R3, tt);
+      tb0.load_prefetched(nb);
+      ge_niels_cneg(nb, e0 < 0);
+      ge_madd(tt, R3, nb);
+      ge_p1p1_to_p3(R3, tt);
+      tb1.load_prefetched(nb);
+      ge_niels_cneg(nb, e1 < 0);
+      ge_madd(tt, R3, nb);
+    }
+    ge_p1p1_to_p2(R2, tt);
+  }
+  AT2V_PHASE(4);
+  // V == identity: X = 0 and Y = Z
+  fe d;
+  fe_sub(d, R2.Y, R2.Z);
+  return ok & fe_iszero(R2.X) & fe_iszero(d);
 }
 
 }  // namespace at2v

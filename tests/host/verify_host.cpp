@@ -51,6 +51,32 @@ struct HostTabB16 {
   void load_prefetched(ge_niels& n) const { n = t[pending]; }
 };
 
+// [j 2^128]B, j = 0..2^15, incrementally from the affine Niels form of [2^128]B
+struct HostTabB16Hi {
+  std::vector<ge_niels> t;
+  mutable int pending = 0;
+  HostTabB16Hi() {
+    t.resize((1 << 15) + 1);
+    const uint32_t s128[8] = {0, 0, 0, 0, 1, 0, 0, 0};
+    ge_p2 Q;
+    ge_scalarmult_base(Q, s128, HostTabB8());
+    ge_niels N1;
+    ge_p2_to_niels(N1, Q);
+    ge_p3 P;
+    ge_p3_identity(P);
+    for (size_t j = 0; j < t.size(); ++j) {
+      ge_p2 q;
+      ge_p3_to_p2(q, P);
+      ge_p2_to_niels(t[j], q);
+      ge_p1p1 r;
+      ge_madd(r, P, N1);
+      ge_p1p1_to_p3(P, r);
+    }
+  }
+  void prefetch(int e) const { pending = e; }
+  void load_prefetched(ge_niels& n) const { n = t[pending]; }
+};
+
 static void words(uint32_t w[8], const uint8_t* b) {
   for (int i = 0; i < 8; ++i) w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
@@ -69,6 +95,7 @@ int main(int argc, char** argv) {
   (void)ok;
   size_t bad_d = 0, bad_s = 0;
   int limit = argc > 2 ? atoi(argv[2]) : (int)n;
+  const int half = argc > 3 ? atoi(argv[3]) : 0;  // 1: the half-size equation (verify_half)
   for (size_t i = 0; i < n && (int)i < limit; ++i) {
     uint32_t R[8], A[8], S[8];
     words(R, &sig[64 * i]);
@@ -82,10 +109,18 @@ int main(int argc, char** argv) {
       return v;
     };
     static HostTabB16 tb;
-    HostTabA ta;
-    auto rl = [&](uint32_t r[8]) { for (int q = 0; q < 8; ++q) r[q] = R[q]; };
-    int d = verify_core<16>(R, A, S, len, mw, POLICY_DALEK_V1, ta, tb, rl);
-    int s = verify_core<16>(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tb, rl);
+    HostTabA ta, tr;
+    int d, s;
+    if (half) {
+      static HostTabB16Hi tb1;
+      auto one = [](int v) { return v; };
+      d = verify_half(R, A, S, len, mw, POLICY_DALEK_V1, ta, tr, tb, tb1, one);
+      s = verify_half(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tr, tb, tb1, one);
+    } else {
+      auto rl = [&](uint32_t r[8]) { for (int q = 0; q < 8; ++q) r[q] = R[q]; };
+      d = verify_core<16>(R, A, S, len, mw, POLICY_DALEK_V1, ta, tb, rl);
+      s = verify_core<16>(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, ta, tb, rl);
+    }
     if (d != vd[i]) { if (bad_d < 10) fprintf(stderr, "dalek mismatch i=%zu cls=%d got=%d want=%d\n", i, cls[i], d, vd[i]); ++bad_d; }
     if (s != vs[i]) { if (bad_s < 10) fprintf(stderr, "sodium mismatch i=%zu cls=%d got=%d want=%d\n", i, cls[i], s, vs[i]); ++bad_s; }
   }

@@ -20,10 +20,13 @@ def host_exe():
     return EXE
 
 
+@pytest.mark.parametrize("half", [0, 1], ids=["full_length", "half_size"])
 @pytest.mark.parametrize("name", golden_io.SETS)
-def test_host_build_of_device_core_matches_golden(host_exe, name):
-    out = subprocess.run([host_exe, os.path.join(golden_io.GOLDEN_DIR, name + ".bin")], capture_output=True,
-                         text=True, timeout=600)
+def test_host_build_of_device_core_matches_golden(host_exe, name, half):
+    """both verify equations the kernel can be built with: the full-length ladder (verify_core) and the
+    half-size lattice form (verify_half, the default), against OpenSSL/libsodium-derived verdicts"""
+    out = subprocess.run([host_exe, os.path.join(golden_io.GOLDEN_DIR, name + ".bin"), "1000000", str(half)],
+                         capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     n, bad_d, bad_s = map(int, out.stdout.split())
     assert bad_d == 0 and bad_s == 0 and n > 0

@@ -1,7 +1,8 @@
 // Phase breakdown of the verify kernel on gfx950: the product kernel (at2v_kernels.hip, included
 // verbatim) built with AT2V_PHASE(k) = "lane 0 adds the s_memtime delta since the previous mark to
-// bucket k of its wave". Buckets: 0 loop/pair overhead, 1 loads + V1 + decompress A, 2 SHA-512 + mod l +
-// recode, 3 A table, 4 ladder, 5 pair inversion, 6 encode + compare + verdict store.
+// bucket k of its wave". Buckets (full-length path): 0 loop/pair overhead, 1 loads + V1 + decompress A,
+// 2 SHA-512 + mod l + recode, 3 A table, 4 ladder, 5 group inversion, 6 encode + compare + verdict store;
+// (half-size path): 1 adds decoding R, 2 adds the lattice reduction, 3 builds both tables, 6 = identity check.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I at2-node_amd/csrc tools/phase_bench.hip -o tools/phase_bench
 #include <hip/hip_runtime.h>
 
@@ -79,8 +80,13 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(hv.data(), ver, hv.size() * 4, hipMemcpyDeviceToHost));
   size_t valid = 0;
   for (uint32_t i = 0; i < n; ++i) valid += (hv[i / 32] >> (i % 32)) & 1;
+#if AT2V_VERIFY_HALF
+  const char* names[8] = {"loop overhead", "loads+V1+decode A,R", "t = c1 s mod l + recode", "A,R tables",
+                          "ladder", "sha512 + mod l", "identity check+store", "lattice reduction"};
+#else
   const char* names[8] = {"pair/loop overhead", "loads+V1+decompress", "sha512+mod l+recode", "A table",
                           "ladder", "group inversion", "encode+compare+store", "-"};
+#endif
   double tot = 0, b[8] = {0};
   const int waves = grid * 4;
   for (int w = 0; w < waves; ++w)
@@ -89,7 +95,7 @@ int main(int argc, char** argv) {
   printf("n=%u grid=%d waves=%d kernel %.3f ms -> %.2f M verifies/s, valid %zu/%u\n", n, grid, waves, ms,
          n / ms / 1e3, valid, n);
   const double chunks = (double)n / 64;
-  for (int k = 0; k < 7; ++k)
+  for (int k = 0; k < 8; ++k)
     printf("  %-24s %6.2f %%   %10.0f wave-cycles per 64-record chunk\n", names[k], 100 * b[k] / tot, b[k] / chunks);
   printf("  total                    %10.0f wave-cycles per chunk (s_memtime; 2 waves share a SIMD)\n", tot / chunks);
   return valid == n ? 0 : 2;
