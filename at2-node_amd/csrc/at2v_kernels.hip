@@ -1,13 +1,13 @@
 // at2v_kernels.hip — gfx950 kernels: batch verify (the hot path) and the GPU record generator / signer.
 //
-// Verify kernel layout:
+// Verify kernel layout (the full-length form of §4 is the AT2V_VERIFY_HALF=0 build):
 //   * one lane = one signature; a wave owns a contiguous chunk of 64 records, so the verdict bits of a
 //     chunk are one __ballot -> two uint32 words written by lane 0 (no atomics, no cross-wave traffic);
-//   * persistent grid (resident waves only), chunks c = wave_id + k * total_waves taken in pairs that
-//     share one field inversion; each wave reuses a fixed 98 KiB slice of the scratch buffer for its 64
-//     per-lane tables [0..8](-A) (cached form, 160 B each, lane-contiguous) and the parked R' of a pair;
-//   * the fixed-base table [0..2^15]B (affine Niels, 128 B per entry, 4.2 MB) is built once per context
-//     and stays L2/MALL-resident; A and B entries reach the lanes through LDS-DMA prefetches;
+//   * persistent grid (resident waves only), chunks c = wave_id + k * total_waves; each wave reuses a
+//     fixed 180 KiB slice of the scratch buffer for its 64 lanes' tables [0..8]A and [0..8](+-R) (cached
+//     form, 160 B per entry, lane-contiguous);
+//   * the fixed-base tables [0..2^15]B and [0..2^15] 2^128 B (affine Niels, 128 B per entry, 8.4 MB) are
+//     built once per context and stay L2/MALL-resident; table entries reach the lanes by LDS-DMA;
 //   * records are read straight from the ABI layout (pk n x 32, sig n x 64, msg + offsets) with
 //     16-byte loads for A/R/S and 4-byte loads + v_alignbit for unaligned message words.
 #include <hip/hip_runtime.h>

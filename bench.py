@@ -20,13 +20,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
 
 CFG_SEED = 0x4154325F
-# Algorithmic work per verify: the verify path performs 1474 field multiplications and
-# 1390 field squarings (decompress 255S+22M, A table 64M, ladder 1008S+1379M, half of one pair
-# inversion 127S+7M, encode 2M); a 10-limb radix-2^25.5 multiplication is 100 and a squaring 55
-# 32x32->64 multiply-accumulates.
-FIELD_MUL_PER_VERIFY = 1474
-FIELD_SQ_PER_VERIFY = 1390
-MAC_PER_VERIFY = 100 * FIELD_MUL_PER_VERIFY + 55 * FIELD_SQ_PER_VERIFY  # 223,850
+# Algorithmic work per verify (half-size equation, 33-window chain): decode A and R
+# 510 S + 44 M, tables [j]A and [j](+-R) 128 M, ladder 32 x (16 S + 28 M) + top window 15 M + 8 fixed-base
+# windows x 14 M = 512 S + 1023 M; 1195 M + 1022 S in all. A 10-limb radix-2^25.5 multiplication is 100 and a
+# squaring 55 32x32->64 multiply-accumulates. (About 17% of waves need a 34th window, +2.1% work: the figure
+# below is the lower bound, so the reported fraction is conservative.)
+FIELD_MUL_PER_VERIFY = 1195
+FIELD_SQ_PER_VERIFY = 1022
+MAC_PER_VERIFY = 100 * FIELD_MUL_PER_VERIFY + 55 * FIELD_SQ_PER_VERIFY  # 175,710
 # Peak: v_mad_i64_i32 issues at half the VALU rate on gfx950 (profiles/r01_ubench_valu.txt): one wave64
 # instruction per 4 cycles per SIMD = 16 lane-MACs/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz.
 MAC_PEAK = 256 * 4 * 16 * 2.4e9  # 3.93e13 MAC/s
