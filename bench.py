@@ -67,7 +67,11 @@ def main():
             raise SystemExit("run N>1 under torch.distributed.run (one process per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # N > 1: one process per GPU, RCCL over xGMI. Under torch.distributed.run at N = 1 the same
+    # process-group path runs too (nccl init, all-gather of the verdict words, barriers, MAX reduce), so a
+    # one-GPU box rehearses the multi-rank code exactly; plain `python bench.py` stays collective-free.
+    use_dist = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     n, L = args.records_per_gpu, args.msg_len
@@ -81,7 +85,7 @@ def main():
     d_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
     words = n // 32
     d_ver = torch.zeros(words, dtype=torch.int32, device=dev)
-    d_all = torch.zeros(words * world, dtype=torch.int32, device=dev) if world > 1 else None
+    d_all = torch.zeros(words * world, dtype=torch.int32, device=dev) if use_dist else None
     # distinct records per rank (indices rank*n .. rank*n+n-1)
     v.gen_records_device(CFG_SEED, rank * n, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
                          d_off.data_ptr(), s)
@@ -90,13 +94,13 @@ def main():
     def step():
         v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
                               d_ver.data_ptr(), s)
-        if world > 1:
+        if use_dist:
             at2dist.gather_verdicts(d_ver, world)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -109,24 +113,24 @@ def main():
         v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
                               d_ver.data_ptr(), s)
         kev[k][1].record(stream)
-        if world > 1:
+        if use_dist:
             d_all = at2dist.gather_verdicts(d_ver, world)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps
     t_dev = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(t_dev, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms = t_dev.tolist()
 
     # verdict check after the timed region: every generated record must be valid, on every rank
-    full = d_all if world > 1 else d_ver
+    full = d_all if use_dist else d_ver
     match = float((full == -1).float().mean().item())
-    if world > 1:
+    if use_dist:
         mt = torch.tensor([match], dtype=torch.float64, device=dev)
         dist.all_reduce(mt, op=dist.ReduceOp.MIN)
         match = mt.item()
@@ -158,7 +162,7 @@ def main():
                 "records_per_gpu": n,
                 "msg_len": L,
                 "policy": args.policy,
-                "parallelism": f"index-shard x{world}" + (" + RCCL all-gather of verdict words" if world > 1 else ""),
+                "parallelism": f"index-shard x{world}" + (" + RCCL all-gather of verdict words" if use_dist else ""),
             },
             "verdict_match": match,
             "kernel_ms": kernel_ms,
@@ -179,7 +183,7 @@ def main():
         }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args, d_pk, d_sig, d_msg, n, L)
-    if rank == 0 and world == 1 and args.pmc_traffic:
+    if rank == 0 and world == 1 and args.pmc_traffic and not use_dist:
         tr = pmc_traffic(args, n, L)
         if tr is not None:
             out["roofline"]["traffic"] = tr["bytes_per_launch"]
@@ -190,7 +194,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     v.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 
