@@ -282,8 +282,28 @@ def pmc_valu(args, n, L):
             "valu_lane_ops_per_verify": lane_ops / n, "valu_lane_ops_per_s": lane_ops / t,
             "frac_full_rate_peak_2400mhz": lane_ops / t / (1024 * 32 * 2.4e9),
             "effective_clock_ghz": clk / 1e9, "issue_frac_nominal": issue, "kernel_s_profiled": t,
+            "valu_busy": valu_busy(args, n, L),
             "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 GRBM_GUI_ACTIVE "
                       "--kernel-trace, one pass, child run (profiled passes clock a few % lower)"}
+
+
+def valu_busy(args, n, L):
+    """SURVEY 8(d) 'VALU-busy', rocprofv3's derived VALUBusy = 100 * sum(SQ_ACTIVE_INST_VALU) / CU_NUM /
+    max(GRBM_GUI_ACTIVE) (its gfx94x formula; ROCm 7.2 has no gfx950 derived-counter section, MI355X guide),
+    plus VALUUtilization = 100 * SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64) (active-lane share).
+    One more PMC pass. GRBM_GUI_ACTIVE arrives summed over the 8 XCDs; its max is the per-XCD value."""
+    r = _pmc_pass(args, n, L, ["SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "GRBM_GUI_ACTIVE"])
+    if r is None:
+        return None
+    c, _ = r
+    gui = c["GRBM_GUI_ACTIVE"] / 8
+    act = c["SQ_ACTIVE_INST_VALU"]
+    return {"valu_busy_pct": 100.0 * act / 256 / gui,
+            "valu_utilization_pct": 100.0 * c["SQ_THREAD_CYCLES_VALU"] / (act * 64) if act else None,
+            "sq_active_inst_valu": act, "sq_thread_cycles_valu": c["SQ_THREAD_CYCLES_VALU"],
+            "grbm_gui_active_per_xcd": gui,
+            "method": "rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace, "
+                      "one pass, child run; rocprofv3 VALUBusy/VALUUtilization formulas"}
 
 
 def cpu_baseline(args, d_pk, d_sig, d_msg, n, L):
