@@ -28,6 +28,7 @@ hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_to
 hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStream_t stream);
 hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs);
 size_t scratch_bytes_per_block();
+size_t scratch_bytes(int grid);
 int block_threads();
 }  // namespace at2v
 
@@ -96,7 +97,7 @@ int init_shard(Shard& s, int device) {
   if (s.blocks_per_cu < 1) s.blocks_per_cu = 1;
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-  AT2V_TRY(s.scratch.ensure((size_t)s.grid * at2v::scratch_bytes_per_block()));
+  AT2V_TRY(s.scratch.ensure(at2v::scratch_bytes(s.grid)));
   // fixed-base table [0..2^(AT2V_BWIN-1)]B, built on the device once per context
   AT2V_TRY(s.btab.ensure(at2v::btab_bytes()));
   AT2V_TRY(at2v::launch_build_btab((int4*)s.btab.p, s.stream));

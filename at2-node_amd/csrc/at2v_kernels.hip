@@ -205,7 +205,7 @@ __device__ AT2V_INLINE int wave_max_i32(int v) {
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   const int lane = threadIdx.x & 63;
@@ -220,7 +220,13 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   const DevTabB tb0{btab, astage + wib * 640, lane};                      // [j]B, staged where A's entry was
   const DevTabB tb1{btab + (size_t)kBtabEntries * 8, rstage + wib * 640, lane};  // [j 2^128]B, in R's stage
   auto wmax = [](int v) { return wave_max_i32(v); };
-  for (uint32_t c = wave; c < nchunks; c += nwaves) {
+  // Chunk c = wave first, then chunks nwaves + ticket from the per-launch queue counter (zeroed by the
+  // launcher). The two waves of a SIMD do not get equal issue shares (arbitration by priority, then age), so
+  // with a static c += nwaves split half the waves finished at 60% of the kernel time and their SIMDs ran the
+  // rest on one wave at half throughput (tools/phase_bench wave timeline). Pulling chunks keeps
+  // both waves busy until the queue drains. The ticket is a vector atomic from lane 0, broadcast with
+  // readfirstlane, so the loop stays wavefront-uniform; every wave leaves after one ticket >= the chunk count.
+  for (uint32_t c = wave; c < nchunks;) {
     AT2V_PHASE(0);
     const uint32_t i = c * 64 + lane;
     const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
@@ -240,10 +246,14 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     };
     const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax) & (i < n);
     const uint64_t mask = __ballot(good);
+    uint32_t ticket = 0;
     if (lane == 0) {
       verdicts[2 * c] = (uint32_t)mask;
       if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
+      ticket = atomicAdd(chunk_queue, 1u);
     }
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    c = ticket < nchunks ? nwaves + ticket : nchunks;  // no wrap: ticket < nchunks <= 2^26
     AT2V_PHASE(6);
   }
 }
@@ -251,7 +261,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 bstage[kWavesPerBlock * 8 * 64];
   const int lane = threadIdx.x & 63;
@@ -591,8 +601,12 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t need_blocks = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
+  // chunk queue counter: the word after the `grid` blocks' lane slots (scratch_bytes(grid))
+  uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesPerBlock);
+  const hipError_t me = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+  if (me != hipSuccess) return me;
   hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                     verdicts, scratch, btab);
+                     verdicts, scratch, btab, queue);
   return hipGetLastError();
 }
 
@@ -628,6 +642,8 @@ hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs) {
 }
 
 size_t scratch_bytes_per_block() { return kScratchPerWave * kWavesPerBlock; }
+// device scratch of a context launching `grid` blocks: their lane slots + the chunk queue counter
+size_t scratch_bytes(int grid) { return (size_t)grid * scratch_bytes_per_block() + 256; }
 int block_threads() { return kBlock; }
 
 }  // namespace at2v

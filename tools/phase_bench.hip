@@ -8,14 +8,22 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #define AT2V_MAX_WAVES 4096
 __device__ unsigned long long at2v_phase_acc[AT2V_MAX_WAVES][8];
 __device__ unsigned long long at2v_phase_last[AT2V_MAX_WAVES];
+// first and last mark of every wave on the constant-rate, device-wide wall clock (s_memrealtime, 100 MHz):
+// the spread of wave end times is the kernel's tail (waves idle while the slowest finish)
+__device__ unsigned long long at2v_wave_t0[AT2V_MAX_WAVES];
+__device__ unsigned long long at2v_wave_t1[AT2V_MAX_WAVES];
 __device__ __forceinline__ void at2v_phase_mark(int k) {
   const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if ((threadIdx.x & 63) == 0 && w < AT2V_MAX_WAVES) {
+    const unsigned long long wt = wall_clock64();
+    if (at2v_wave_t0[w] == 0) at2v_wave_t0[w] = wt;
+    at2v_wave_t1[w] = wt;
     const unsigned long long t = clock64();
     if (k > 0) at2v_phase_acc[w][k] += t - at2v_phase_last[w];
     else if (at2v_phase_last[w]) at2v_phase_acc[w][0] += t - at2v_phase_last[w];
@@ -55,7 +63,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&msg, (size_t)n * L));
   CHECK(hipMalloc(&off, (size_t)(n + 1) * 4));
   CHECK(hipMalloc(&ver, (size_t)(n + 31) / 32 * 4));
-  CHECK(hipMalloc(&scratch, (size_t)grid * at2v::scratch_bytes_per_block()));
+  CHECK(hipMalloc(&scratch, at2v::scratch_bytes(grid)));
   CHECK(hipMalloc(&btab, at2v::btab_bytes()));
   CHECK(at2v::launch_build_btab(btab, 0));
   CHECK(at2v::launch_gen(0x4154325F, 0, n, L, pk, sig, msg, off, 0));
@@ -65,6 +73,8 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 2; ++rep) {
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_acc), zero.data(), zero.size() * 8));
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_last), zl.data(), zl.size() * 8));
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_wave_t0), zl.data(), zl.size() * 8));
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_wave_t1), zl.data(), zl.size() * 8));
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
@@ -98,5 +108,31 @@ int main(int argc, char** argv) {
   for (int k = 0; k < 8; ++k)
     printf("  %-24s %6.2f %%   %10.0f wave-cycles per 64-record chunk\n", names[k], 100 * b[k] / tot, b[k] / chunks);
   printf("  total                    %10.0f wave-cycles per chunk (s_memtime; 2 waves share a SIMD)\n", tot / chunks);
+  {
+    std::vector<unsigned long long> t0(AT2V_MAX_WAVES), t1(AT2V_MAX_WAVES);
+    CHECK(hipMemcpyFromSymbol(t0.data(), HIP_SYMBOL(at2v_wave_t0), t0.size() * 8));
+    CHECK(hipMemcpyFromSymbol(t1.data(), HIP_SYMBOL(at2v_wave_t1), t1.size() * 8));
+    unsigned long long s0 = ~0ull, s1 = 0, e0 = ~0ull, e1 = 0;
+    std::vector<double> ends;
+    double life = 0;
+    for (int w = 0; w < waves; ++w) {
+      if (!t0[w]) continue;
+      s0 = t0[w] < s0 ? t0[w] : s0;
+      s1 = t0[w] > s1 ? t0[w] : s1;
+      e0 = t1[w] < e0 ? t1[w] : e0;
+      e1 = t1[w] > e1 ? t1[w] : e1;
+    }
+    for (int w = 0; w < waves; ++w)
+      if (t0[w]) {
+        ends.push_back((double)(t1[w] - s0));
+        life += (double)(t1[w] - t0[w]);
+      }
+    std::sort(ends.begin(), ends.end());
+    const double span = (double)(e1 - s0), m = ends.size();
+    printf("wave timeline (100 MHz wall clock, us from the first wave's first mark): start spread %.1f us; end min %.1f "
+           "p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f; mean wave life / span = %.4f\n",
+           (s1 - s0) / 100.0, ends[0] / 100, ends[(size_t)(0.1 * m)] / 100, ends[(size_t)(0.5 * m)] / 100,
+           ends[(size_t)(0.9 * m)] / 100, ends[(size_t)(0.99 * m)] / 100, span / 100, life / m / span);
+  }
   return valid == n ? 0 : 2;
 }
