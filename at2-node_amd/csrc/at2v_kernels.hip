@@ -33,8 +33,21 @@ namespace at2v {
 #define AT2V_INV_GROUP 2  // chunks whose final inversions share one field inversion (Montgomery's trick)
 #endif
 
-constexpr int kBlock = 256;
+#ifndef AT2V_BLOCK
+#define AT2V_BLOCK 512  // verify threads per block: 8 waves, both waves of every SIMD in one workgroup
+#endif
+#ifndef AT2V_QUEUE
+#define AT2V_QUEUE 1  // 1: chunks after the first come from the per-launch queue; 0: static c += nwaves
+#endif
+#ifndef AT2V_FAIR
+#define AT2V_FAIR 1  // 1: the two waves of a SIMD pace each other with s_setprio (needs AT2V_BLOCK 512)
+#endif
+constexpr int kBlock = AT2V_BLOCK;
 constexpr int kWavesPerBlock = kBlock / 64;
+static_assert(!AT2V_FAIR || kBlock == 512, "pacing pairs waves w and w^4 of an 8-wave workgroup");
+// control words after the lane slots of a launch's `grid` blocks: [0] chunk queue counter; from word 16 on,
+// one 64-byte progress line per wave (AT2V_FAIR)
+constexpr size_t kCtlBytes(int grid) { return 64 + (size_t)grid * kWavesPerBlock * 64; }
 constexpr int kBWin = AT2V_BWIN;
 constexpr int kGroup = AT2V_INV_GROUP;
 static_assert(kGroup >= 1 && kGroup <= 8, "inversion group");
@@ -201,6 +214,29 @@ __device__ AT2V_INLINE int wave_max_i32(int v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+#if AT2V_FAIR
+// Pacing of the two waves that share a SIMD (an 8-wave workgroup places waves w and w^4 on one SIMD;
+// MI355X guide, "Two waves per SIMD"). VALU issue goes by priority, then age, so without it the older wave
+// runs nearly unimpeded and the younger gets leftover slots. Each wave publishes its progress (work units,
+// ~1 per ladder window) and raises its priority while it trails its partner. The partner's value is read
+// one mark late (the load issued at mark k is consumed at mark k+1), so the loads' latency is hidden; a
+// stale value only misjudges one interval. Stores are vector stores from lane 0.
+struct Pace {
+  uint32_t* mine;
+  const uint32_t* mate;
+  uint32_t prog;
+  uint32_t mate_prog;
+  __device__ AT2V_INLINE void mark(uint32_t units) {
+    prog += units;
+    const uint32_t behind = __builtin_amdgcn_readfirstlane(mate_prog > prog ? 1u : 0u);
+    if (behind) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(mine, prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mate_prog = __hip_atomic_load(mate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+#endif
+
 // Half-size verification: one chunk of 64 records per wave, no final inversion.
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -220,6 +256,13 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   const DevTabB tb0{btab, astage + wib * 640, lane};                      // [j]B, staged where A's entry was
   const DevTabB tb1{btab + (size_t)kBtabEntries * 8, rstage + wib * 640, lane};  // [j 2^128]B, in R's stage
   auto wmax = [](int v) { return wave_max_i32(v); };
+#if AT2V_FAIR
+  uint32_t* prog_lines = chunk_queue + 16;
+  Pace pace{prog_lines + (size_t)wave * 16, prog_lines + (size_t)(wave ^ 4) * 16, 0u, 0u};
+  if (lane == 0) __hip_atomic_store(pace.mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  NoPace pace;
+#endif
   // Chunk c = wave first, then chunks nwaves + ticket from the per-launch queue counter (zeroed by the
   // launcher). The two waves of a SIMD do not get equal issue shares (arbitration by priority, then age), so
   // with a static c += nwaves split half the waves finished at 60% of the kernel time and their SIMDs ran the
@@ -244,16 +287,22 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
       const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
       return __builtin_amdgcn_alignbit(hi, lo, sh);
     };
-    const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax) & (i < n);
+    const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
     const uint64_t mask = __ballot(good);
     uint32_t ticket = 0;
     if (lane == 0) {
       verdicts[2 * c] = (uint32_t)mask;
       if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
+#if AT2V_QUEUE
       ticket = atomicAdd(chunk_queue, 1u);
+#endif
     }
+#if AT2V_QUEUE
     ticket = __builtin_amdgcn_readfirstlane(ticket);
     c = ticket < nchunks ? nwaves + ticket : nchunks;  // no wrap: ticket < nchunks <= 2^26
+#else
+    c += nwaves;
+#endif
     AT2V_PHASE(6);
   }
 }
@@ -643,7 +692,7 @@ hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs) {
 
 size_t scratch_bytes_per_block() { return kScratchPerWave * kWavesPerBlock; }
 // device scratch of a context launching `grid` blocks: their lane slots + the chunk queue counter
-size_t scratch_bytes(int grid) { return (size_t)grid * scratch_bytes_per_block() + 256; }
+size_t scratch_bytes(int grid) { return (size_t)grid * scratch_bytes_per_block() + kCtlBytes(grid); }
 int block_threads() { return kBlock; }
 
 }  // namespace at2v

@@ -234,10 +234,14 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
 //   TabP : store(e, cached) / prefetch(e) / load_prefetched(cached)   (per lane, e in 0..8)
 //   TabB : prefetch(e) / load_prefetched(niels)                       (shared, e in 0..2^15)
 //   WaveMax : int(int) -> maximum over the lanes that verify together (identity on the host)
-template <class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax>
+//   Pace : mark(units) after each phase and ladder window (progress, ~1 unit per window; NoPace = none)
+struct NoPace {
+  AT2V_HD AT2V_INLINE void mark(uint32_t) {}
+};
+template <class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax, class Pace = NoPace>
 AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                     MsgWord msgword, int policy, TabP& ta, TabP& tr, const TabB0& tb0,
-                                    const TabB1& tb1, WaveMax wave_max) {
+                                    const TabB1& tb1, WaveMax wave_max, Pace&& pace = Pace()) {
   // V1: s < l
   int ok = sc_is_canonical(Sw);
   if (policy == POLICY_LIBSODIUM_1_0_18) {
@@ -251,6 +255,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
   ok &= ge_frombytes(R, Rw);
   ok &= !(fe_iszero(R.X) & (int)(Rw[7] >> 31));
   AT2V_PHASE(1);
+  pace.mark(10);
   // V3: k = SHA-512(R || A || M) mod l
   uint32_t k[8];
   {
@@ -267,10 +272,12 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
     sc_reduce512(k, hw);
   }
   AT2V_PHASE(5);
+  pace.mark(3);
   // half-size scalars
   HalfScalars hs;
   lattice_reduce(hs, k);
   AT2V_PHASE(7);
+  pace.mark(3);
   uint32_t t[8];
   sc_mul_signed(t, hs, Sw);
   uint32_t c0d[8], c1d[8], td[8];
@@ -281,6 +288,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
   int nw = wave_max(nw_lane);
   nw = nw < 29 ? 29 : nw;  // B digits sit at windows 0, 4, ..., 28
   AT2V_PHASE(2);
+  pace.mark(1);
 
   // tables [j]A and [j](+-R), j = 0..8
   if (hs.c1_neg) {
@@ -306,6 +314,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
     }
   }
   AT2V_PHASE(3);
+  pace.mark(4);
 
   // shared doubling chain over windows nw-1 .. 0:
   //   acc = 16 acc + a_i A + r_i (+-R) + [4 | i, i < 32] (-t_{i/4} [2^(16 i/4)]B - t_{8+i/4} [2^(128+16 i/4)]B)
@@ -331,6 +340,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
     ge_p1p1_to_p2(R2, tt);
   }
   for (int i = nw - 2; i >= 0; --i) {
+    pace.mark(1);
     const int da = digit4(c0d, i), dr = digit4(c1d, i);
     ta.prefetch(da < 0 ? -da : da);  // both land while the window's four doublings run
     tr.prefetch(dr < 0 ? -dr : dr);

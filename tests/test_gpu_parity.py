@@ -57,7 +57,9 @@ def test_golden_libsodium_policy(verifier_sodium, golden, name):
 
 def test_info(verifier):
     info = verifier.info()
-    assert info["cus"] >= 1 and info["grid_blocks"] >= info["cus"] and info["block_threads"] == 256
+    # 8-wave blocks (both waves of every SIMD in one workgroup, paced), one per CU: 2 waves/SIMD
+    assert info["cus"] >= 1 and info["grid_blocks"] >= info["cus"] and info["block_threads"] == 512
+    assert info["grid_blocks"] * info["block_threads"] // 64 == 8 * info["cus"]
 
 
 @pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 63, 64, 65, 127, 1000])

@@ -51,7 +51,8 @@ int main(int argc, char** argv) {
   int bpc = 0, vg = 0;
   CHECK(at2v::verify_occupancy(&bpc, &vg));
   const int grid = prop.multiProcessorCount * bpc;
-  if (grid * 4 > AT2V_MAX_WAVES) {
+  const int wpb = at2v::block_threads() / 64;
+  if (grid * wpb > AT2V_MAX_WAVES) {
     printf("grid too large\n");
     return 1;
   }
@@ -98,7 +99,7 @@ int main(int argc, char** argv) {
                           "ladder", "group inversion", "encode+compare+store", "-"};
 #endif
   double tot = 0, b[8] = {0};
-  const int waves = grid * 4;
+  const int waves = grid * wpb;
   for (int w = 0; w < waves; ++w)
     for (int k = 0; k < 8; ++k) b[k] += (double)acc[w * 8 + k];
   for (int k = 0; k < 8; ++k) tot += b[k];
