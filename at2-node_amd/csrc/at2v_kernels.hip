@@ -269,7 +269,12 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   // rest on one wave at half throughput (tools/phase_bench wave timeline). Pulling chunks keeps
   // both waves busy until the queue drains. The ticket is a vector atomic from lane 0, broadcast with
   // readfirstlane, so the loop stays wavefront-uniform; every wave leaves after one ticket >= the chunk count.
-  for (uint32_t c = wave; c < nchunks;) {
+  // First chunks: waves 0..3 of every block (one per SIMD) come before waves 4..7, so a launch with at most
+  // 4 chunks per block runs every chunk on a SIMD of its own (blocks take the whole LDS: one per CU).
+  constexpr uint32_t kHalf = kWavesPerBlock / 2;
+  const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
+                                            : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
+  for (uint32_t c = c_first; c < nchunks;) {
     AT2V_PHASE(0);
     const uint32_t i = c * 64 + lane;
     const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
@@ -648,7 +653,7 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
                          const int4* btab, int grid, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint32_t nchunks = (n + 63) / 64;
-  const uint32_t need_blocks = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint32_t need_blocks = (nchunks + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);  // half-filled blocks
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
   // chunk queue counter: the word after the `grid` blocks' lane slots (scratch_bytes(grid))
   uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesPerBlock);
