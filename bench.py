@@ -52,6 +52,11 @@ def parse():
 
 def main():
     args = parse()
+    # stdout carries exactly one line, the JSON result: everything else that writes to fd 1 (RCCL's version
+    # banner at communicator init, library chatter) is sent to stderr.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -192,7 +197,8 @@ def main():
         if vl is not None:
             out["roofline"]["valu_measured"] = vl
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     v.close()
     if use_dist:
         dist.barrier()
