@@ -39,6 +39,9 @@ namespace at2v {
 #ifndef AT2V_QUEUE
 #define AT2V_QUEUE 1  // 1: chunks after the first come from the per-launch queue; 0: static c += nwaves
 #endif
+#ifndef AT2V_SOLO_TAIL
+#define AT2V_SOLO_TAIL 0  // 1: waves 4..7 stop pulling chunks for the last nwaves/2 chunks of a launch
+#endif
 #ifndef AT2V_FAIR
 #define AT2V_FAIR 1  // 1: the two waves of a SIMD pace each other with s_setprio (needs AT2V_BLOCK 512)
 #endif
@@ -221,14 +224,27 @@ __device__ AT2V_INLINE int wave_max_i32(int v) {
 // ~1 per ladder window) and raises its priority while it trails its partner. The partner's value is read
 // one mark late (the load issued at mark k is consumed at mark k+1), so the loads' latency is hidden; a
 // stale value only misjudges one interval. Stores are vector stores from lane 0.
+#ifndef AT2V_FAIR_LAG
+#define AT2V_FAIR_LAG -1  // >= 0: half-window progress units, the younger half trails its partner by this many
+#endif
 struct Pace {
   uint32_t* mine;
   const uint32_t* mate;
   uint32_t prog;
   uint32_t mate_prog;
-  __device__ AT2V_INLINE void mark(uint32_t units) {
+  int lag;  // 0 for waves 0..3; AT2V_FAIR_LAG for waves 4..7 (their target lead is negative)
+#if AT2V_FAIR_LAG >= 0
+  __device__ AT2V_INLINE void mark(uint32_t units) { step(2 * units); }
+  __device__ AT2V_INLINE void window() { step(1); }
+  __device__ AT2V_INLINE void mid() { step(1); }
+#else
+  __device__ AT2V_INLINE void mark(uint32_t units) { step(units); }
+  __device__ AT2V_INLINE void window() { step(1); }
+  __device__ AT2V_INLINE void mid() {}
+#endif
+  __device__ AT2V_INLINE void step(uint32_t units) {
     prog += units;
-    const uint32_t behind = __builtin_amdgcn_readfirstlane(mate_prog > prog ? 1u : 0u);
+    const uint32_t behind = __builtin_amdgcn_readfirstlane((int)(mate_prog - prog) > lag ? 1u : 0u);
     if (behind) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     if ((threadIdx.x & 63) == 0) __hip_atomic_store(mine, prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -258,7 +274,8 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   auto wmax = [](int v) { return wave_max_i32(v); };
 #if AT2V_FAIR
   uint32_t* prog_lines = chunk_queue + 16;
-  Pace pace{prog_lines + (size_t)wave * 16, prog_lines + (size_t)(wave ^ 4) * 16, 0u, 0u};
+  Pace pace{prog_lines + (size_t)wave * 16, prog_lines + (size_t)(wave ^ 4) * 16, 0u, 0u,
+            (wib >= 4 && AT2V_FAIR_LAG > 0) ? AT2V_FAIR_LAG : 0};
   if (lane == 0) __hip_atomic_store(pace.mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
   NoPace pace;
@@ -299,7 +316,15 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
       verdicts[2 * c] = (uint32_t)mask;
       if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
 #if AT2V_QUEUE
-      ticket = atomicAdd(chunk_queue, 1u);
+#if AT2V_SOLO_TAIL
+      // the last nwaves/2 chunks go to waves 0..3 only: their SIMD partners leave, so each of those chunks
+      // runs on one wave per SIMD instead of ending as a partnerless straggler
+      if (wib >= (int)kHalf &&
+          __hip_atomic_load(chunk_queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + nwaves + nwaves / 2 >= nchunks)
+        ticket = nchunks;
+      else
+#endif
+        ticket = atomicAdd(chunk_queue, 1u);
 #endif
     }
 #if AT2V_QUEUE

@@ -234,9 +234,12 @@ AT2V_HD AT2V_INLINE int verify_core(const uint32_t Rw[8], const uint32_t Aw[8], 
 //   TabP : store(e, cached) / prefetch(e) / load_prefetched(cached)   (per lane, e in 0..8)
 //   TabB : prefetch(e) / load_prefetched(niels)                       (shared, e in 0..2^15)
 //   WaveMax : int(int) -> maximum over the lanes that verify together (identity on the host)
-//   Pace : mark(units) after each phase and ladder window (progress, ~1 unit per window; NoPace = none)
+//   Pace : mark(units) after each phase, window() at each ladder window start, mid() after its doublings
+//          (progress, ~1 unit per window; NoPace = none)
 struct NoPace {
   AT2V_HD AT2V_INLINE void mark(uint32_t) {}
+  AT2V_HD AT2V_INLINE void window() {}
+  AT2V_HD AT2V_INLINE void mid() {}
 };
 template <class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax, class Pace = NoPace>
 AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
@@ -340,7 +343,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
     ge_p1p1_to_p2(R2, tt);
   }
   for (int i = nw - 2; i >= 0; --i) {
-    pace.mark(1);
+    pace.window();
     const int da = digit4(c0d, i), dr = digit4(c1d, i);
     ta.prefetch(da < 0 ? -da : da);  // both land while the window's four doublings run
     tr.prefetch(dr < 0 ? -dr : dr);
@@ -350,6 +353,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
     }
     ge_p2_dbl(tt, R2);
     ge_p1p1_to_p3(R3, tt);
+    pace.mid();
     const bool bwin = (i & 3) == 0 && i < 32;
     int e0 = 0, e1 = 0;
     if (bwin) {  // -t digits j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B)
