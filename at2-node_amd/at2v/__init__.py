@@ -2,7 +2,8 @@
 
 Thin plumbing over the C ABI in include/at2v.h, used by the tests and bench.py. The product is the
 HIP library. This module has NO CPU fallback: if libat2v.so or a gfx950 device is missing, every
-call raises.
+batch call raises. ``verify_one`` is the per-signature entry point, a CPU function by contract
+(SURVEY §8(b)), not a fallback.
 
 Reference interface mirrored (drop::crypto::sign, used by at2-node at src/lib.rs:5,19,
 src/client.rs:72-78, src/bin/server/rpc.rs:269,281):
@@ -29,8 +30,10 @@ _POLICIES = {"dalek": POLICY_DALEK_V1, "dalek_v1": POLICY_DALEK_V1, "libsodium":
 
 # must match include/at2v.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = ("at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
-                    "at2v_verify_one", "at2v_strerror", "at2v_gen_records_device", "at2v_sign_batch",
-                    "at2v_get_info", "at2v_decode_points",
+                    "at2v_verify_one", "at2v_verify_one_policy", "at2v_strerror", "at2v_gen_records_device",
+                    "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
+                    "at2v_comm_get_unique_id", "at2v_comm_init_rank", "at2v_verify_shard_gather_device",
+                    "at2v_verify_batch_sharded",
                     "at2v_queue_create", "at2v_queue_destroy", "at2v_queue_submit", "at2v_queue_flush",
                     "at2v_queue_poll", "at2v_queue_get_stats", "at2v_queue_reset_latency",
                     "at2v_pack_send_asset",
@@ -55,7 +58,11 @@ class _Opts(ctypes.Structure):
 
 class _Info(ctypes.Structure):
     _fields_ = [("num_gpus", ctypes.c_int), ("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
-                ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int), ("vgprs", ctypes.c_int)]
+                ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int), ("vgprs", ctypes.c_int),
+                ("rank", ctypes.c_int), ("world", ctypes.c_int)]
+
+
+UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)
 
 
 _lib = None
@@ -87,6 +94,17 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.at2v_verify_batch_device.restype = ctypes.c_int
     lib.at2v_verify_one.argtypes = [P, P, P, ctypes.c_size_t]
     lib.at2v_verify_one.restype = ctypes.c_int
+    lib.at2v_verify_one_policy.argtypes = [P, P, P, ctypes.c_size_t, ctypes.c_int]
+    lib.at2v_verify_one_policy.restype = ctypes.c_int
+    lib.at2v_comm_get_unique_id.argtypes = [P]
+    lib.at2v_comm_get_unique_id.restype = ctypes.c_int
+    lib.at2v_comm_init_rank.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
+    lib.at2v_comm_init_rank.restype = ctypes.c_int
+    lib.at2v_verify_shard_gather_device.argtypes = [P, P, P, P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.c_size_t,
+                                                    P, P]
+    lib.at2v_verify_shard_gather_device.restype = ctypes.c_int
+    lib.at2v_verify_batch_sharded.argtypes = [P, P, P, P, P, ctypes.c_size_t, P]
+    lib.at2v_verify_batch_sharded.restype = ctypes.c_int
     lib.at2v_strerror.argtypes = [ctypes.c_int]
     lib.at2v_strerror.restype = ctypes.c_char_p
     lib.at2v_gen_records_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
@@ -193,6 +211,37 @@ class BatchVerifier:
         _check(self._lib.at2v_verify_batch_device(self._h, d_pk, d_sig, d_msg, msg_bytes, d_off, n, d_verdicts,
                                                   stream or None), "at2v_verify_batch_device")
 
+    # ---- one rank per GPU: RCCL all-gather of the verdict words (include/at2v.h)
+    def comm_init_rank(self, unique_id: bytes, rank: int, world: int) -> None:
+        """Attach an RCCL communicator (collective over `world` processes; unique_id from comm_unique_id() on
+        rank 0, shared out of band)."""
+        if len(unique_id) != UNIQUE_ID_BYTES:
+            raise ValueError("unique id must be %d bytes" % UNIQUE_ID_BYTES)
+        _check(self._lib.at2v_comm_init_rank(self._h, bytes(unique_id), rank, world), "at2v_comm_init_rank")
+
+    def verify_shard_gather_device(self, d_pk: int, d_sig: int, d_msg: int, msg_bytes: int, d_off: int,
+                                   n_local: int, words_per_rank: int, d_bitmap: int, stream: int = 0) -> None:
+        """verify this rank's n_local device records into its slice of d_bitmap, then all-gather (asynchronous)"""
+        _check(self._lib.at2v_verify_shard_gather_device(self._h, d_pk or None, d_sig or None, d_msg or None,
+                                                         msg_bytes, d_off or None, n_local, words_per_rank,
+                                                         d_bitmap, stream or None),
+               "at2v_verify_shard_gather_device")
+
+    def verify_batch_sharded(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, msg_off: np.ndarray) -> np.ndarray:
+        """the node batch (same on every rank) -> bool[n] verdicts of the whole batch on every rank"""
+        pk = np.ascontiguousarray(pk, dtype=np.uint8)
+        sig = np.ascontiguousarray(sig, dtype=np.uint8)
+        msg = np.ascontiguousarray(msg, dtype=np.uint8).reshape(-1)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        n = len(msg_off) - 1
+        if pk.size != 32 * n or sig.size != 64 * n:
+            raise ValueError("pk/sig/msg_off sizes disagree")
+        words = np.zeros(max(1, (n + 31) // 32), dtype=np.uint32)
+        msg_arg = msg if msg.size else np.zeros(1, np.uint8)
+        _check(self._lib.at2v_verify_batch_sharded(self._h, _ptr(pk), _ptr(sig), _ptr(msg_arg), _ptr(msg_off), n,
+                                                   _ptr(words)), "at2v_verify_batch_sharded")
+        return unpack_verdicts(words, n)
+
     def gen_records_device(self, cfg_seed: int, first: int, n: int, msg_len: int, d_pk: int, d_sig: int, d_msg: int,
                            d_off: Optional[int], stream: int = 0) -> None:
         _check(self._lib.at2v_gen_records_device(self._h, cfg_seed, first, n, msg_len, d_pk, d_sig, d_msg,
@@ -219,12 +268,20 @@ class BatchVerifier:
         return pk, sig
 
 
-def verify_one(pk: bytes, sig: bytes, msg: bytes) -> bool:
+def comm_unique_id() -> bytes:
+    """RCCL unique id for at2v_comm_init_rank (rank 0 creates it; hand it to the other ranks out of band)"""
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(load_library().at2v_comm_get_unique_id(buf), "at2v_comm_get_unique_id")
+    return buf.raw
+
+
+def verify_one(pk: bytes, sig: bytes, msg: bytes, policy="dalek") -> bool:
+    """One signature on the CPU (at2v_verify_one: the product's verify code built for the host; no GPU)."""
     lib = load_library()
-    a = np.frombuffer(pk, np.uint8)
-    s = np.frombuffer(sig, np.uint8)
-    m = np.frombuffer(msg, np.uint8) if msg else np.zeros(1, np.uint8)
-    return bool(_check(lib.at2v_verify_one(_ptr(a), _ptr(s), _ptr(m), len(msg)), "at2v_verify_one"))
+    if len(pk) != 32 or len(sig) != 64:
+        raise ValueError("public key must be 32 bytes and signature 64 bytes")
+    return bool(_check(lib.at2v_verify_one_policy(bytes(pk), bytes(sig), bytes(msg) if msg else None, len(msg),
+                                                  _POLICIES[policy]), "at2v_verify_one_policy"))
 
 
 # ------------------------------------------------ drop::crypto::sign mirror
@@ -258,6 +315,7 @@ class Signature:
         self.bytes = bytes(data)
 
     def verify(self, message: bytes, public_key: PublicKey) -> None:
-        """Raise VerifyError unless the signature is valid (GPU path; no CPU fallback)."""
+        """Raise VerifyError unless the signature is valid (at2v_verify_one: the per-signature CPU entry point,
+        as drop's synchronous verify is; batches go through BatchVerifier on the GPU)."""
         if not verify_one(public_key.bytes, self.bytes, bytes(message)):
             raise VerifyError("signature verification failed")

@@ -26,6 +26,34 @@ PACK_OK, PACK_BAD_RECIPIENT, PACK_BAD_SENDER, PACK_BAD_SIGNATURE = 0, 1, 2, 3
 INITIAL_BALANCE = 100000  # accounts/account.rs:17
 
 
+VERDICT_INVALID, VERDICT_VALID, VERDICT_FAILED = 0, 1, 0xFF  # at2v_queue_poll verdict bytes (at2v.h)
+
+
+class BatchFailedError(RuntimeError):
+    """Verdicts from a batch that failed on the device (at2v_queue_poll reports 0xff for each of its records).
+    Nothing from such a batch may be treated as verified: the caller re-submits it or drops it."""
+
+
+def verdict_mask(verdicts, n: int) -> np.ndarray:
+    """Per-record verdicts -> bool[n] of VALID records, failing closed.
+
+    Accepts bool[n], or integers [n] that are each 0 (invalid) or 1 (valid) — the queue's uint8 verdicts.
+    A 0xff (failed batch) raises BatchFailedError; any other value raises ValueError. Only == 1 counts as
+    valid, so a device failure can never turn into an approval."""
+    v = np.asarray(verdicts)
+    if v.shape != (n,):
+        raise ValueError(f"expected {n} per-record verdicts, got shape {v.shape}")
+    if v.dtype == bool:
+        return v.copy()
+    if not np.issubdtype(v.dtype, np.integer):
+        raise ValueError(f"verdicts must be bool or integer, not {v.dtype}")
+    if (v == VERDICT_FAILED).any():
+        raise BatchFailedError(f"{int((v == VERDICT_FAILED).sum())} records come from a batch that failed on the device")
+    if ((v != VERDICT_INVALID) & (v != VERDICT_VALID)).any():
+        raise ValueError("per-record verdicts must be 0 or 1")
+    return v == VERDICT_VALID
+
+
 class AccountError(Exception):
     """accounts::Error::AccountModification { source: account::Error } (accounts/mod.rs:16-18)."""
 
@@ -153,7 +181,9 @@ class IngestQueue:
         _chk(self._lib.at2v_queue_flush(self._h), "at2v_queue_flush")
 
     def poll(self, max_items: int = 65536, timeout_us: int = 0):
-        """-> (tickets u64[k], verdicts u8[k]) in ticket order"""
+        """-> (tickets u64[k], verdicts u8[k]) in ticket order; a verdict is 1 (valid), 0 (invalid) or 0xff
+        (its batch failed on the device: not verified either way). Turn them into a valid-mask with
+        verdict_mask(), which refuses 0xff, never with astype(bool)."""
         t = np.zeros(max_items, np.uint64)
         v = np.zeros(max_items, np.uint8)
         k = _chk(self._lib.at2v_queue_poll(self._h, _p(t), _p(v), max_items, timeout_us), "at2v_queue_poll")
@@ -278,8 +308,12 @@ class Ledger:
                                 t.state) for t in buf[:k]]
 
     def deliver(self, sender: np.ndarray, sequence: np.ndarray, recipient: np.ndarray, amount: np.ndarray,
-                verdicts: Optional[np.ndarray] = None, now_us: int = 0) -> dict:
-        """One delivered batch; `verdicts` = verify verdict words (bit i%32 of word i/32) or bool[n], None = all"""
+                verdicts: Optional[np.ndarray] = None, now_us: int = 0, words: Optional[np.ndarray] = None) -> dict:
+        """One delivered batch. Which records were verified is given by exactly one of
+          * `verdicts`: per-record bool[n] or 0/1 integers (the queue's uint8 verdicts; 0xff = failed batch
+            raises BatchFailedError before anything is applied — see verdict_mask);
+          * `words`: the verify call's uint32 verdict bitmap (bit i%32 of word i/32), ceil(n/32) words;
+          * neither: every record is delivered."""
         sender = np.ascontiguousarray(sender, np.uint8).reshape(-1, 32)
         n = len(sender)
         seq = np.ascontiguousarray(sequence, np.uint32)
@@ -287,14 +321,17 @@ class Ledger:
         amt = np.ascontiguousarray(amount, np.uint64)
         if len(seq) != n or len(rcp) != n or len(amt) != n:
             raise ValueError("field lengths disagree")
-        words = None
+        if verdicts is not None and words is not None:
+            raise ValueError("give per-record verdicts or bitmap words, not both")
         if verdicts is not None:
-            v = np.asarray(verdicts)
-            if v.dtype == bool or (v.dtype == np.uint8 and v.size == n):
-                words = np.packbits(v.astype(np.uint8), bitorder="little")
-                words = np.concatenate([words, np.zeros((-len(words)) % 4, np.uint8)]).view("<u4")
-            else:
-                words = np.ascontiguousarray(v, "<u4")
+            ok = verdict_mask(verdicts, n)
+            words = np.packbits(ok.astype(np.uint8), bitorder="little")
+            words = np.concatenate([words, np.zeros((-len(words)) % 4, np.uint8)]).view("<u4")
+        elif words is not None:
+            w = np.asarray(words)
+            if w.dtype not in (np.uint32, np.int32) or w.shape != ((n + 31) // 32,):
+                raise ValueError(f"bitmap words must be {(n + 31) // 32} uint32/int32 words")
+            words = np.ascontiguousarray(w).view("<u4")
         st = _ApplyStats()
         _chk(self._lib.at2v_ledger_deliver(self._h, _p(sender), _p(seq), _p(rcp), _p(amt),
                                            _p(words) if words is not None else None, n, now_us, ctypes.byref(st)),

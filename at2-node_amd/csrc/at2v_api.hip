@@ -4,7 +4,16 @@
 // and growable device staging buffers for host batches. Host batches are split by index range
 // (aligned to 64 records = one wave chunk = two verdict words) across the context's devices;
 // each shard runs H2D -> verify -> D2H on its own stream, so shards overlap.
+//
+// Every verify launch of a context goes through launch_shard(): launches take turns on the device's
+// scratch (an event recorded after each launch, waited on by the next one, whatever stream either is on),
+// and the verdict words are zeroed before the kernel, so a chunk that no wave wrote fails closed.
+//
+// Multi-process (one rank per GPU): at2v_comm_init_rank attaches an RCCL communicator to a
+// context; at2v_verify_shard_gather_device / at2v_verify_batch_sharded verify this rank's index range and
+// ncclAllGather the verdict words over xGMI, so every rank holds the node bitmap (rpc.rs:156-173 consumer).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -57,6 +66,7 @@ struct DevBuf {
 struct Shard {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t scratch_free = nullptr;  // recorded after every verify launch: the next one waits on it
   int grid = 0;  // persistent grid (blocks)
   int cus = 0;
   int blocks_per_cu = 0;
@@ -69,6 +79,9 @@ struct Shard {
 struct at2v_ctx {
   at2v_policy policy = AT2V_POLICY_DALEK_V1;
   std::vector<Shard> shards;
+  ncclComm_t comm = nullptr;  // at2v_comm_init_rank (one rank per process, the context's first device)
+  int rank = 0, world = 1;
+  DevBuf bitmap;              // node bitmap of at2v_verify_batch_sharded (world x words_per_rank words)
 };
 
 namespace {
@@ -97,6 +110,8 @@ int init_shard(Shard& s, int device) {
   if (s.blocks_per_cu < 1) s.blocks_per_cu = 1;
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free, hipEventDisableTiming));
+  AT2V_TRY(hipEventRecord(s.scratch_free, s.stream));
   AT2V_TRY(s.scratch.ensure(at2v::scratch_bytes(s.grid)));
   // fixed-base table [0..2^(AT2V_BWIN-1)]B, built on the device once per context
   AT2V_TRY(s.btab.ensure(at2v::btab_bytes()));
@@ -106,6 +121,28 @@ int init_shard(Shard& s, int device) {
 }
 
 bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+// One verify launch on shard s (current device = s.device), on `stream`. Launches of a context take turns
+// on the shard's scratch (per-wave tables, chunk-queue counter, pacing lines): this one waits for the
+// previous one, on whatever stream that ran. The verdict words are zeroed first (fail closed).
+hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                        uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream) {
+  hipError_t e = hipStreamWaitEvent(stream, s.scratch_free, 0);
+  if (e == hipSuccess) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
+  if (e == hipSuccess)
+    e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch.p,
+                            (const int4*)s.btab.p, s.grid, stream);
+  if (e == hipSuccess) e = hipEventRecord(s.scratch_free, stream);
+  return e;
+}
+
+int nccl_code(ncclResult_t r) { return r == ncclSuccess ? AT2V_OK : AT2V_E_RCCL; }
+
+// contiguous, 64-aligned, equal padded shards (at2v/dist.py shard_bounds)
+size_t shard_per_rank(size_t n, int world) {
+  const size_t per = (n + (size_t)world - 1) / (size_t)world;
+  return (per + 63) / 64 * 64;
+}
 
 }  // namespace
 
@@ -142,9 +179,17 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
 
 void at2v_destroy(at2v_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->comm) {
+    (void)hipSetDevice(ctx->shards.empty() ? 0 : ctx->shards[0].device);
+    (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ctx->bitmap.release();
   for (Shard& s : ctx->shards) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.scratch_free) (void)hipEventSynchronize(s.scratch_free);
+    if (s.scratch_free) (void)hipEventDestroy(s.scratch_free);
     s.scratch.release();
     s.btab.release();
     s.pk.release();
@@ -202,9 +247,8 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
       e = hipMemcpyAsync(s.msg.p, msg + mb0, mbytes, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(s.off.p, offs.data(), (m + 1) * 4, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
-      e = at2v::launch_verify((const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
-                              (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (int)ctx->policy,
-                              (uint32_t*)s.verdict.p, (int4*)s.scratch.p, (const int4*)s.btab.p, s.grid, s.stream);
+      e = launch_shard(ctx, s, (const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
+                       (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (uint32_t*)s.verdict.p, s.stream);
     // a = multiple of 64 => the shard's words start at word a/32
     if (e == hipSuccess)
       e = hipMemcpyAsync(verdicts + a / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, s.stream);
@@ -235,30 +279,114 @@ int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* 
   (void)hipGetDevice(&prev);
   hipError_t e = hipSetDevice(s.device);
   if (e == hipSuccess)
-    e = at2v::launch_verify(d_pk, d_sig, d_msg, (uint32_t)msg_bytes, d_msg_off, (uint32_t)n, (int)ctx->policy,
-                            d_verdicts, (int4*)s.scratch.p, (const int4*)s.btab.p, s.grid, (hipStream_t)hip_stream);
+    e = launch_shard(ctx, s, d_pk, d_sig, d_msg, (uint32_t)msg_bytes, d_msg_off, (uint32_t)n, d_verdicts,
+                     (hipStream_t)hip_stream);
   (void)hipSetDevice(prev);
   return hip_code(e);
 }
 
-static std::mutex g_one_mu;
-static at2v_ctx* g_one_ctx = nullptr;
+// ---- RCCL: one rank per process ----
 
-int at2v_verify_one(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len) {
-  if (!pk || !sig || (!msg && len) || len >= (1ull << 31)) return AT2V_E_INVALID;
-  std::lock_guard<std::mutex> lk(g_one_mu);
-  if (!g_one_ctx) {
-    int rc = at2v_create(nullptr, &g_one_ctx);
-    if (rc != AT2V_OK) {
-      g_one_ctx = nullptr;
-      return rc;
+int at2v_comm_get_unique_id(uint8_t out[AT2V_UNIQUE_ID_BYTES]) {
+  if (!out) return AT2V_E_INVALID;
+  static_assert(AT2V_UNIQUE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return AT2V_E_RCCL;
+  std::memcpy(out, id.internal, AT2V_UNIQUE_ID_BYTES);
+  return AT2V_OK;
+}
+
+int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BYTES], int rank, int world) {
+  if (!ctx || !unique_id || world < 1 || rank < 0 || rank >= world || ctx->comm || ctx->shards.size() != 1)
+    return AT2V_E_INVALID;
+  ncclUniqueId id;
+  std::memcpy(id.internal, unique_id, AT2V_UNIQUE_ID_BYTES);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  int rc = hip_code(hipSetDevice(ctx->shards[0].device));
+  if (rc == AT2V_OK) rc = nccl_code(ncclCommInitRank(&ctx->comm, world, id, rank));
+  if (rc == AT2V_OK) {
+    ctx->rank = rank;
+    ctx->world = world;
+  } else {
+    ctx->comm = nullptr;
+  }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int at2v_verify_shard_gather_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                                    size_t msg_bytes, const uint32_t* d_msg_off, size_t n_local,
+                                    size_t words_per_rank, uint32_t* d_bitmap, void* hip_stream) {
+  if (!ctx || !ctx->comm || !d_bitmap || words_per_rank == 0 || n_local > 32 * words_per_rank ||
+      words_per_rank >= (1ull << 26) || (n_local && (!d_pk || !d_sig || !d_msg_off)) || msg_bytes >= (1ull << 32))
+    return AT2V_E_INVALID;
+  if (!aligned(d_bitmap, 4) || (n_local && (!aligned(d_pk, 16) || !aligned(d_sig, 16) || !aligned(d_msg_off, 4))))
+    return AT2V_E_ALIGN;
+  Shard& s = ctx->shards[0];
+  const hipStream_t st = (hipStream_t)hip_stream;
+  uint32_t* mine = d_bitmap + (size_t)ctx->rank * words_per_rank;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(s.device);
+  // pad words of this rank's slice are 0 (and the whole slice if n_local == 0)
+  if (e == hipSuccess) e = hipMemsetAsync(mine, 0, words_per_rank * 4, st);
+  if (e == hipSuccess && n_local)
+    e = launch_shard(ctx, s, d_pk, d_sig, d_msg, (uint32_t)msg_bytes, d_msg_off, (uint32_t)n_local, mine, st);
+  int rc = hip_code(e);
+  // in place: rank r's send buffer is recvbuff + r * count
+  if (rc == AT2V_OK) rc = nccl_code(ncclAllGather(mine, d_bitmap, words_per_rank, ncclUint32, ctx->comm, st));
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                              const uint32_t* msg_off, size_t n, uint32_t* verdicts) {
+  if (!ctx || !ctx->comm || n >= (1u << 31)) return AT2V_E_INVALID;
+  if (n && (!pk || !sig || !msg_off || !verdicts || (!msg && msg_off[n] != msg_off[0]))) return AT2V_E_INVALID;
+  Shard& s = ctx->shards[0];
+  const size_t per = shard_per_rank(n ? n : 1, ctx->world), wpr = per / 32;
+  const size_t a = std::min(n, (size_t)ctx->rank * per), b = std::min(n, a + per), m = b - a;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(s.device);
+  std::vector<uint32_t> offs(m + 1);
+  const uint32_t mb0 = m ? msg_off[a] : 0;
+  for (size_t i = 0; i <= m; ++i) {
+    offs[i] = m ? msg_off[a + i] - mb0 : 0;
+    if (i && offs[i] < offs[i - 1]) e = hipErrorInvalidValue;
+  }
+  const size_t mbytes = m ? offs[m] : 0;
+  if (e == hipSuccess) e = ctx->bitmap.ensure(wpr * (size_t)ctx->world * 4);
+  if (e == hipSuccess && m) {
+    e = s.pk.ensure(m * 32);
+    if (e == hipSuccess) e = s.sig.ensure(m * 64);
+    if (e == hipSuccess) e = s.msg.ensure(mbytes + 16);
+    if (e == hipSuccess) e = s.off.ensure((m + 1) * 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.pk.p, pk + a * 32, m * 32, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.sig.p, sig + a * 64, m * 64, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess && mbytes) e = hipMemcpyAsync(s.msg.p, msg + mb0, mbytes, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.off.p, offs.data(), (m + 1) * 4, hipMemcpyHostToDevice, s.stream);
+  }
+  int rc = e == hipErrorInvalidValue ? AT2V_E_INVALID : hip_code(e);
+  if (rc == AT2V_OK)
+    rc = at2v_verify_shard_gather_device(ctx, (const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
+                                         mbytes, (const uint32_t*)s.off.p, m, wpr, (uint32_t*)ctx->bitmap.p, s.stream);
+  // rank r's words sit at word r * wpr of the padded bitmap: copy each rank's slice to its place in verdicts
+  if (rc == AT2V_OK && n) {
+    (void)hipSetDevice(s.device);
+    for (int r = 0; r < ctx->world && rc == AT2V_OK; ++r) {
+      const size_t ra = std::min(n, (size_t)r * per), rb = std::min(n, ra + per);
+      if (rb <= ra) break;
+      const size_t words = (rb - ra + 31) / 32;  // ra is a multiple of 64: its words start at ra / 32
+      rc = hip_code(hipMemcpyAsync(verdicts + ra / 32, (uint32_t*)ctx->bitmap.p + (size_t)r * wpr, words * 4,
+                                   hipMemcpyDeviceToHost, s.stream));
     }
   }
-  uint32_t off[2] = {0, (uint32_t)len};
-  uint32_t verdict = 0;
-  static const uint8_t empty[1] = {0};
-  int rc = at2v_verify_batch(g_one_ctx, pk, sig, len ? msg : empty, off, 1, &verdict);
-  return rc < 0 ? rc : (int)(verdict & 1u);
+  if (rc == AT2V_OK) rc = hip_code(hipStreamSynchronize(s.stream));
+  (void)hipSetDevice(prev);
+  return rc;
 }
 
 const char* at2v_strerror(int code) {
@@ -361,6 +489,8 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
   out->waves_per_cu = s.blocks_per_cu * at2v::block_threads() / 64;
   out->cus = s.cus;
   out->vgprs = s.vgprs;
+  out->rank = ctx->rank;
+  out->world = ctx->comm ? ctx->world : 0;
   return AT2V_OK;
 }
 

@@ -1,7 +1,7 @@
 // at2v_fe_base.h — GF(2^255-19) element, radix 2^25.5, 10 balanced signed int32 limbs.
 //
-// Compiles for gfx950 (hipcc) and for the host (g++, used only by the CPU unit test of the
-// field layer, tests/test_fe_host.py). Design and bound proof: DESIGN.md §3, tools/gen_fe.py.
+// Compiles for gfx950 (hipcc) and for the host (g++: at2v_verify_one in at2v_cpu.cpp, and the CPU tests
+// tests/test_host_core.py / test_verify_one_cpu.py). Design and bound proof: DESIGN.md §3, tools/gen_fe.py.
 //
 // Bound classes used by the curve formulas (at2v_ge.h):
 //   carried  : |v_i| <= 2^(w_i-1) (+2^16 on limb 1)   — output of fe_mul/fe_sq/fe_carry32/fe_frombytes

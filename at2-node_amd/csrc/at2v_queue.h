@@ -82,11 +82,16 @@ class BatchQueue {
     return 0;
   }
 
-  // Seals what is pending, waits until every launched batch has completed, joins the threads.
+  // Seals what is pending, waits until every launched batch has completed, joins the threads, frees the
+  // slots. Also frees what a start() that failed part-way had allocated (no threads were started then).
   void stop() {
     {
       std::unique_lock<std::mutex> lk(m_);
-      if (!running_) return;
+      if (!running_) {
+        lk.unlock();
+        release_slots();
+        return;
+      }
       flush_req_ = true;
       cv_launch_.notify_all();
       cv_idle_.wait(lk, [&] { return (!fill_ || fill_->n == 0) && ready_.empty() && !launching_ && inflight_.empty(); });
@@ -96,7 +101,7 @@ class BatchQueue {
     cv_complete_.notify_all();
     launcher_.join();
     completer_.join();
-    for (auto& s : slots_) be_.release(s);
+    release_slots();
   }
 
   // Append n records (ABI layout; msg_off has n+1 entries, message i = msg[off[i]..off[i+1])).
@@ -216,6 +221,13 @@ class BatchQueue {
     bool failed;
     std::vector<uint32_t> words;
   };
+
+  // every slot that start() touched, including a partly allocated one (release() skips null buffers)
+  void release_slots() {
+    for (auto& s : slots_) be_.release(s);
+    slots_.clear();
+    free_.clear();
+  }
 
   void seal_locked() {
     ready_.push_back(fill_);

@@ -287,7 +287,11 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
   sc_recode4_hi8(c0d, hs.c0);
   sc_recode4_hi8(c1d, hs.c1);
   sc_recode16(td, t);
-  const int nw_lane = ok ? hs.bits / 4 + 1 : 0;  // windows for values < 2^(4 nw - 1)
+  // 64 signed radix-16 digits hold values < 2^255. The reduction returns max(|c0|, |c1|) <= max(k, ~2^128) < 2^253
+  // (tests/test_lattice_host.py), so this guard never fires; if it did, the lane fails closed
+  // instead of running a 65th window on a truncated digit string.
+  ok &= hs.bits <= 255;
+  const int nw_lane = ok ? hs.bits / 4 + 1 : 0;  // windows for values < 2^(4 nw - 1); <= 64
   int nw = wave_max(nw_lane);
   nw = nw < 29 ? 29 : nw;  // B digits sit at windows 0, 4, ..., 28
   AT2V_PHASE(2);

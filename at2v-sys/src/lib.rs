@@ -1,0 +1,288 @@
+//! at2v-sys — raw bindings of `include/at2v.h` (libat2v: MI355X batch Ed25519 verification for at2-node)
+//! plus a thin safe layer for the two call shapes the server needs.
+//!
+//! Where it plugs into the reference (/root/reference, at2-node v1):
+//!   * per payload, as the body of drop's `Signature::verify` that sieve/murmur call for every payload
+//!     broadcast at src/bin/server/rpc.rs:275-284 -> `verify_one` (CPU, reentrant);
+//!   * per gossiped batch, ahead of `deliver()` at rpc.rs:156-173 -> `BatchVerifier::verify` (GPU) or the
+//!     ingest queue (`at2v_queue_*`);
+//!   * one process per GPU: `at2v_comm_init_rank` + `at2v_verify_batch_sharded` (RCCL all-gather of the
+//!     verdict bitmap over xGMI).
+//! The extern block below must stay identical to include/at2v.h (names, argument counts, integer widths);
+//! tests/test_sys_crate.py checks it, since this image cannot run cargo.
+#![allow(non_camel_case_types)]
+
+use std::os::raw::{c_char, c_int, c_long, c_void};
+
+// ---------------------------------------------------------------- types and constants (at2v.h)
+
+#[repr(C)]
+pub struct At2vCtx {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct At2vQueue {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct At2vLedger {
+    _private: [u8; 0],
+}
+
+pub const AT2V_POLICY_DALEK_V1: c_int = 0;
+pub const AT2V_POLICY_LIBSODIUM_1_0_18: c_int = 1;
+
+pub const AT2V_OK: c_int = 0;
+pub const AT2V_E_INVALID: c_int = -1;
+pub const AT2V_E_NODEVICE: c_int = -2;
+pub const AT2V_E_HIP: c_int = -3;
+pub const AT2V_E_OOM: c_int = -4;
+pub const AT2V_E_ALIGN: c_int = -5;
+pub const AT2V_E_RCCL: c_int = -6;
+
+pub const AT2V_UNIQUE_ID_BYTES: usize = 128;
+
+pub const AT2V_WIRE_BYTES: c_int = 0;
+pub const AT2V_WIRE_ARRAY: c_int = 1;
+pub const AT2V_PACK_OK: u8 = 0;
+pub const AT2V_PACK_BAD_RECIPIENT: u8 = 1;
+pub const AT2V_PACK_BAD_SENDER: u8 = 2;
+pub const AT2V_PACK_BAD_SIGNATURE: u8 = 3;
+
+pub const AT2V_TX_OK: c_int = 0;
+pub const AT2V_TX_INCONSECUTIVE_SEQUENCE: c_int = 1;
+pub const AT2V_TX_OVERFLOW: c_int = 2;
+pub const AT2V_TX_UNDERFLOW: c_int = 3;
+pub const AT2V_TX_PENDING: i32 = 0;
+pub const AT2V_TX_SUCCESS: i32 = 1;
+pub const AT2V_TX_FAILURE: i32 = 2;
+
+/// at2v_queue_poll verdict bytes
+pub const AT2V_VERDICT_INVALID: u8 = 0;
+pub const AT2V_VERDICT_VALID: u8 = 1;
+pub const AT2V_VERDICT_FAILED: u8 = 0xff;
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct At2vOpts {
+    pub device: c_int,
+    pub num_gpus: c_int,
+    pub policy: c_int,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct At2vInfo {
+    pub num_gpus: c_int,
+    pub grid_blocks: c_int,
+    pub block_threads: c_int,
+    pub waves_per_cu: c_int,
+    pub cus: c_int,
+    pub vgprs: c_int,
+    pub rank: c_int,
+    pub world: c_int,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct At2vQueueOpts {
+    pub device: c_int,
+    pub policy: c_int,
+    pub max_batch: u32,
+    pub max_delay_us: u32,
+    pub max_msg_bytes: u32,
+    pub depth: u32,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct At2vQueueStats {
+    pub submitted: u64,
+    pub completed: u64,
+    pub batches: u64,
+    pub failed_batches: u64,
+    pub mean_batch: f64,
+    pub p50_us: f64,
+    pub p99_us: f64,
+    pub max_us: f64,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct At2vSendAssetRequest {
+    pub sender: *const u8,
+    pub sender_len: usize,
+    pub sequence: u32,
+    pub recipient: *const u8,
+    pub recipient_len: usize,
+    pub amount: u64,
+    pub signature: *const u8,
+    pub signature_len: usize,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct At2vFullTransaction {
+    pub timestamp_us: u64,
+    pub sender: [u8; 32],
+    pub sender_sequence: u32,
+    pub recipient: [u8; 32],
+    pub amount: u64,
+    pub state: i32,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct At2vApplyStats {
+    pub delivered: u64,
+    pub rejected: u64,
+    pub applied: u64,
+    pub requeued: u64,
+    pub expired: u64,
+    pub passes: u64,
+}
+
+// ---------------------------------------------------------------- functions (at2v.h, same order)
+
+extern "C" {
+    pub fn at2v_create(opts: *const At2vOpts, out: *mut *mut At2vCtx) -> c_int;
+    pub fn at2v_destroy(ctx: *mut At2vCtx);
+    pub fn at2v_verify_batch(ctx: *mut At2vCtx, pk: *const u8, sig: *const u8, msg: *const u8, msg_off: *const u32,
+                             n: usize, verdicts: *mut u32) -> c_int;
+    pub fn at2v_verify_batch_device(ctx: *mut At2vCtx, d_pk: *const u8, d_sig: *const u8, d_msg: *const u8,
+                                    msg_bytes: usize, d_msg_off: *const u32, n: usize, d_verdicts: *mut u32,
+                                    hip_stream: *mut c_void) -> c_int;
+    pub fn at2v_verify_one(pk: *const u8, sig: *const u8, msg: *const u8, len: usize) -> c_int;
+    pub fn at2v_verify_one_policy(pk: *const u8, sig: *const u8, msg: *const u8, len: usize, policy: c_int) -> c_int;
+    pub fn at2v_strerror(code: c_int) -> *const c_char;
+    pub fn at2v_gen_records_device(ctx: *mut At2vCtx, cfg_seed: u64, first: u64, n: usize, msg_len: u32,
+                                   d_pk: *mut u8, d_sig: *mut u8, d_msg: *mut u8, d_msg_off: *mut u32,
+                                   hip_stream: *mut c_void) -> c_int;
+    pub fn at2v_sign_batch(ctx: *mut At2vCtx, seeds: *const u8, msg: *const u8, msg_off: *const u32, n: usize,
+                           pk_out: *mut u8, sig_out: *mut u8) -> c_int;
+    pub fn at2v_get_info(ctx: *mut At2vCtx, out: *mut At2vInfo) -> c_int;
+
+    pub fn at2v_comm_get_unique_id(out: *mut u8) -> c_int;
+    pub fn at2v_comm_init_rank(ctx: *mut At2vCtx, unique_id: *const u8, rank: c_int, world: c_int) -> c_int;
+    pub fn at2v_verify_shard_gather_device(ctx: *mut At2vCtx, d_pk: *const u8, d_sig: *const u8, d_msg: *const u8,
+                                           msg_bytes: usize, d_msg_off: *const u32, n_local: usize,
+                                           words_per_rank: usize, d_bitmap: *mut u32, hip_stream: *mut c_void)
+                                           -> c_int;
+    pub fn at2v_verify_batch_sharded(ctx: *mut At2vCtx, pk: *const u8, sig: *const u8, msg: *const u8,
+                                     msg_off: *const u32, n: usize, verdicts: *mut u32) -> c_int;
+
+    pub fn at2v_queue_create(opts: *const At2vQueueOpts, out: *mut *mut At2vQueue) -> c_int;
+    pub fn at2v_queue_destroy(q: *mut At2vQueue);
+    pub fn at2v_queue_submit(q: *mut At2vQueue, pk: *const u8, sig: *const u8, msg: *const u8, msg_off: *const u32,
+                             n: usize, first_ticket: *mut u64) -> c_int;
+    pub fn at2v_queue_flush(q: *mut At2vQueue) -> c_int;
+    pub fn at2v_queue_poll(q: *mut At2vQueue, tickets: *mut u64, verdicts: *mut u8, max: usize, timeout_us: u32)
+                           -> c_long;
+    pub fn at2v_queue_get_stats(q: *mut At2vQueue, out: *mut At2vQueueStats) -> c_int;
+    pub fn at2v_queue_reset_latency(q: *mut At2vQueue) -> c_int;
+
+    pub fn at2v_pack_send_asset(req: *const At2vSendAssetRequest, n: usize, wire: c_int, pk_out: *mut u8,
+                                sig_out: *mut u8, msg_out: *mut u8, msg_off_out: *mut u32, recipient_out: *mut u8,
+                                status_out: *mut u8) -> c_long;
+    pub fn at2v_decode_points(ctx: *mut At2vCtx, pts: *const u8, n: usize, valid_words: *mut u32) -> c_int;
+
+    pub fn at2v_ledger_create(out: *mut *mut At2vLedger) -> c_int;
+    pub fn at2v_ledger_destroy(l: *mut At2vLedger);
+    pub fn at2v_ledger_balance(l: *const At2vLedger, pk: *const u8, out: *mut u64) -> c_int;
+    pub fn at2v_ledger_last_sequence(l: *const At2vLedger, pk: *const u8, out: *mut u32) -> c_int;
+    pub fn at2v_ledger_transfer(l: *mut At2vLedger, sender: *const u8, sequence: u32, recipient: *const u8,
+                                amount: u64) -> c_int;
+    pub fn at2v_ledger_recent_put(l: *mut At2vLedger, sender: *const u8, sequence: u32, recipient: *const u8,
+                                  amount: u64, now_us: u64) -> c_int;
+    pub fn at2v_ledger_recent_get(l: *const At2vLedger, out: *mut At2vFullTransaction, max: usize) -> c_long;
+    pub fn at2v_ledger_deliver(l: *mut At2vLedger, sender: *const u8, sequence: *const u32, recipient: *const u8,
+                               amount: *const u64, verdicts: *const u32, n: usize, now_us: u64,
+                               stats: *mut At2vApplyStats) -> c_int;
+    pub fn at2v_ledger_pending(l: *const At2vLedger) -> c_long;
+}
+
+// ---------------------------------------------------------------- safe layer
+
+/// A negative at2v return code (backend failure: no device, HIP, OOM, RCCL). Never "invalid signature".
+#[derive(Debug, Clone, Copy, PartialEq, Eq)]
+pub struct Error(pub c_int);
+
+impl std::fmt::Display for Error {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        let s = unsafe { std::ffi::CStr::from_ptr(at2v_strerror(self.0)) };
+        write!(f, "at2v error {}: {}", self.0, s.to_string_lossy())
+    }
+}
+
+impl std::error::Error for Error {}
+
+fn check(rc: c_int) -> Result<c_int, Error> {
+    if rc < 0 {
+        Err(Error(rc))
+    } else {
+        Ok(rc)
+    }
+}
+
+/// One signature on the CPU, dalek-1.x semantics: the body of drop's per-payload `Signature::verify`.
+/// Reentrant; needs no GPU.
+pub fn verify_one(public_key: &[u8; 32], signature: &[u8; 64], message: &[u8]) -> Result<bool, Error> {
+    let m = if message.is_empty() { std::ptr::null() } else { message.as_ptr() };
+    check(unsafe { at2v_verify_one(public_key.as_ptr(), signature.as_ptr(), m, message.len()) }).map(|v| v == 1)
+}
+
+/// Owner of an at2v context (GPU). Not Sync: one thread at a time; call from `spawn_blocking` or a
+/// dedicated thread, never on an async executor thread.
+pub struct BatchVerifier(*mut At2vCtx);
+
+unsafe impl Send for BatchVerifier {}
+
+impl BatchVerifier {
+    pub fn new(device: i32, num_gpus: i32, policy: c_int) -> Result<Self, Error> {
+        let opts = At2vOpts { device, num_gpus, policy };
+        let mut p = std::ptr::null_mut();
+        check(unsafe { at2v_create(&opts, &mut p) })?;
+        Ok(BatchVerifier(p))
+    }
+
+    /// One process per GPU: join the node's RCCL communicator (collective over `world` ranks).
+    pub fn init_rank(&mut self, unique_id: &[u8; AT2V_UNIQUE_ID_BYTES], rank: i32, world: i32) -> Result<(), Error> {
+        check(unsafe { at2v_comm_init_rank(self.0, unique_id.as_ptr(), rank, world) }).map(|_| ())
+    }
+
+    /// Records in the at2v_verify_batch layout -> one bool per record (bit i of the verdict bitmap).
+    /// `sharded`: every rank passes the same node batch; each verifies its range and the RCCL all-gather
+    /// returns the whole bitmap (requires `init_rank`).
+    pub fn verify(&mut self, pk: &[u8], sig: &[u8], msg: &[u8], msg_off: &[u32], sharded: bool)
+                  -> Result<Vec<bool>, Error> {
+        let n = msg_off.len().saturating_sub(1);
+        if pk.len() != 32 * n || sig.len() != 64 * n {
+            return Err(Error(AT2V_E_INVALID));
+        }
+        let mut words = vec![0u32; (n + 31) / 32];
+        let m = if msg.is_empty() { std::ptr::null() } else { msg.as_ptr() };
+        let rc = unsafe {
+            if sharded {
+                at2v_verify_batch_sharded(self.0, pk.as_ptr(), sig.as_ptr(), m, msg_off.as_ptr(), n,
+                                          words.as_mut_ptr())
+            } else {
+                at2v_verify_batch(self.0, pk.as_ptr(), sig.as_ptr(), m, msg_off.as_ptr(), n, words.as_mut_ptr())
+            }
+        };
+        check(rc)?;
+        Ok((0..n).map(|i| (words[i / 32] >> (i % 32)) & 1 == 1).collect())
+    }
+}
+
+impl Drop for BatchVerifier {
+    fn drop(&mut self) {
+        unsafe { at2v_destroy(self.0) }
+    }
+}
+
+/// RCCL unique id for `BatchVerifier::init_rank` (rank 0 creates it and sends it to the others).
+pub fn unique_id() -> Result<[u8; AT2V_UNIQUE_ID_BYTES], Error> {
+    let mut id = [0u8; AT2V_UNIQUE_ID_BYTES];
+    check(unsafe { at2v_comm_get_unique_id(id.as_mut_ptr()) })?;
+    Ok(id)
+}

@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, RCCL comms */
+typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, and the RCCL
+                                     communicator once at2v_comm_init_rank has attached one */
 
 typedef enum {
   AT2V_POLICY_DALEK_V1 = 0,         /* ed25519-dalek 1.x PublicKey::verify (the reference; default) */
@@ -45,12 +46,15 @@ enum {
   AT2V_E_HIP = -3,      /* HIP runtime error */
   AT2V_E_OOM = -4,      /* device or host allocation failed */
   AT2V_E_ALIGN = -5,    /* device pointer not 16-byte aligned (pk, sig) or 4-byte aligned (offsets, verdicts) */
-  AT2V_E_RCCL = -6      /* RCCL communicator / collective failure (multi-GPU contexts) */
+  AT2V_E_RCCL = -6      /* RCCL communicator / collective failure (at2v_comm_init_rank, the verdict all-gather) */
 };
 
 /* Create / destroy a context. opts may be NULL (device 0, one GPU, DALEK_V1). Replaces nothing in the
  * reference directly: it owns what drop's SystemManager::run(.., num_cpus::get()) workers did
- * implicitly (rpc.rs:124-125). A context is not thread-safe: one thread at a time. */
+ * implicitly (rpc.rs:124-125). A context is not thread-safe: one thread at a time. Its verify launches take
+ * turns on the device scratch in call order, whatever streams they are given (each launch waits for the
+ * previous one of the same context), so launches on different streams never overlap; use one context per
+ * concurrent verifier. */
 int at2v_create(const at2v_opts* opts, at2v_ctx** out);
 void at2v_destroy(at2v_ctx* ctx);
 
@@ -69,15 +73,22 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
 /* Batch verify on device-resident buffers of ctx's first device, asynchronously on `hip_stream`
  * (a hipStream_t; NULL = the null stream). Same layout as at2v_verify_batch; msg_bytes = size of the
  * msg buffer in bytes (>= msg_off[n]); d_pk/d_sig 16-byte aligned, d_msg_off/d_verdicts 4-byte aligned.
- * Returns after the launch; results are valid once the stream reaches this point. */
+ * Returns after the launch; results are valid once the stream reaches this point. The ceil(n/32) verdict
+ * words are zeroed on the stream before the kernel runs. The launch first waits (on the device, not the
+ * host) for the context's previous launch, which may be on another stream. */
 int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                              size_t msg_bytes, const uint32_t* d_msg_off, size_t n, uint32_t* d_verdicts,
                              void* hip_stream);
 
-/* One signature, synchronous: 1 = valid, 0 = invalid, < 0 = error. The drop-in for the
- * per-signature `verify(&message, &public_key)` shape; runs a 1-record batch on a
- * process-wide default context (device 0, DALEK_V1), serialised by an internal mutex. */
+/* One signature on the CPU, synchronous: 1 = valid, 0 = invalid, < 0 = error. The drop-in for the
+ * per-signature `Signature::verify(&message, &public_key)` that drop exposes and sieve/murmur call per payload
+ * ("CPU, 1/0"), for callers that verify one payload at a time, e.g. the A/sig decode at
+ * rpc.rs:265-281. DALEK_V1 semantics, the product's own field/group/scalar headers (csrc/) compiled for the
+ * host; needs no GPU, no context and no lock; reentrant. It is not a fallback of the batch entry points:
+ * they never verify on the CPU. */
 int at2v_verify_one(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len);
+/* Same, with an explicit policy (AT2V_POLICY_*). */
+int at2v_verify_one_policy(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len, int policy);
 
 const char* at2v_strerror(int code);
 
@@ -105,8 +116,32 @@ typedef struct {
   int waves_per_cu;    /* resident waves per CU admitted by the kernel's register/LDS use */
   int cus;             /* compute units of the first device */
   int vgprs;           /* VGPRs per lane of the verify kernel (from the code object) */
+  int rank;            /* at2v_comm_init_rank: this context's rank, else 0 */
+  int world;           /* at2v_comm_init_rank: ranks in the communicator, else 0 */
 } at2v_info;
 int at2v_get_info(at2v_ctx* ctx, at2v_info* out);
+
+/* ---- multi-GPU, one process per GPU: RCCL all-gather of the verdict bitmap ----
+ * A node batch of n records is split by contiguous index range: rank r verifies records
+ * [r*per, min(n, (r+1)*per)) with per = ceil(ceil(n/world)/64)*64, i.e. words_per_rank = per/32 verdict words,
+ * and one ncclAllGather over xGMI gives every rank the node bitmap, which the apply step (rpc.rs:156-173)
+ * consumes. Rank 0 creates the unique id and the caller hands it to the other ranks out of band. */
+#define AT2V_UNIQUE_ID_BYTES 128
+int at2v_comm_get_unique_id(uint8_t out[AT2V_UNIQUE_ID_BYTES]);
+/* Attach an RCCL communicator on ctx's device (single-device contexts only). Collective: blocks until all
+ * `world` ranks have called it. */
+int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BYTES], int rank, int world);
+/* Device buffers, asynchronous on hip_stream: verify this rank's n_local records (<= 32*words_per_rank) into
+ * d_bitmap + rank*words_per_rank (pad words zeroed), then all-gather (in place) so d_bitmap holds
+ * world*words_per_rank words on every rank. Collective: every rank calls it with the same words_per_rank. */
+int at2v_verify_shard_gather_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                                    size_t msg_bytes, const uint32_t* d_msg_off, size_t n_local,
+                                    size_t words_per_rank, uint32_t* d_bitmap, void* hip_stream);
+/* Host buffers, synchronous: every rank passes the SAME node batch (at2v_verify_batch layout); each uploads
+ * and verifies only its own range, the all-gather fills in the rest, and every rank receives all ceil(n/32)
+ * verdict words in record order. Collective. */
+int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                              const uint32_t* msg_off, size_t n, uint32_t* verdicts);
 
 
 /* ---- ingest/batching queue: the server's verify call site ----

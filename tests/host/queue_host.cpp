@@ -1,7 +1,7 @@
 // queue_host.cpp — TEST ONLY: the product's batching queue (at2-node_amd/csrc/at2v_queue.h) driven on
 // the CPU with the oracle as its verify backend, to check flush policy, ticket order and verdict mapping
 // without a GPU. The shipped queue is instantiated with the HIP backend in at2v_host.hip.
-// usage: queue_host <scenario>   scenario in {order, size, deadline, flush, drain}; exit 0 = pass
+// usage: queue_host <scenario>   scenario in {order, size, deadline, flush, drain, startfail, failed}; exit 0 = pass
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -17,15 +17,26 @@ using namespace at2v;
 
 struct OracleBackend {
   std::atomic<int> launches{0};
+  int fail_alloc_at = -1;   // >= 0: the alloc() call with this index fails after taking one buffer
+  int fail_launch_at = -1;  // >= 0: the launch() call with this index reports a device error
+  int allocs = 0, releases = 0, held = 0;  // buffers taken and given back (leak check)
   int alloc(QueueSlot& s) {
+    if (allocs++ == fail_alloc_at) {
+      s.pk = (uint8_t*)malloc(s.cap_records * 32);  // partly allocated slot
+      held += s.pk != nullptr;
+      return -4;
+    }
     s.pk = (uint8_t*)malloc(s.cap_records * 32);
     s.sig = (uint8_t*)malloc(s.cap_records * 64);
     s.msg = (uint8_t*)malloc(s.cap_msg);
     s.off = (uint32_t*)malloc((s.cap_records + 1) * 4);
     s.verdicts = (uint32_t*)malloc((s.cap_records + 31) / 32 * 4);
+    held += 5;
     return (s.pk && s.sig && s.msg && s.off && s.verdicts) ? 0 : -4;
   }
   void release(QueueSlot& s) {
+    ++releases;
+    for (void* p : {(void*)s.pk, (void*)s.sig, (void*)s.msg, (void*)s.off, (void*)s.verdicts}) held -= p != nullptr;
     free(s.pk);
     free(s.sig);
     free(s.msg);
@@ -33,7 +44,7 @@ struct OracleBackend {
     free(s.verdicts);
   }
   int launch(QueueSlot& s) {  // asynchronous, like the HIP backend
-    ++launches;
+    if (launches++ == fail_launch_at) return -3;
     s.backend = new std::thread([&s] {
       oracle_verify_batch(s.pk, s.sig, s.msg, s.off, s.n, ORACLE_POLICY_DALEK_V1, s.verdicts, 2);
     });
@@ -41,6 +52,7 @@ struct OracleBackend {
   }
   int wait(QueueSlot& s) {
     auto* t = static_cast<std::thread*>(s.backend);
+    if (!t) return -3;
     t->join();
     delete t;
     s.backend = nullptr;
@@ -240,6 +252,46 @@ int scenario_drain() {
   return 0;
 }
 
+int scenario_startfail() {
+  // a start() that fails on slot 2 must not leak slots 0, 1 or the partial slot 2
+  OracleBackend be;
+  be.fail_alloc_at = 2;
+  QueueOpts o;
+  o.max_batch = 64;
+  o.depth = 4;
+  {
+    BatchQueue<OracleBackend> q(be, o);
+    REQUIRE(q.start() != 0);
+  }  // destructor -> stop()
+  printf("startfail allocs=%d releases=%d held=%d\n", be.allocs, be.releases, be.held);
+  REQUIRE(be.allocs == 3 && be.held == 0);
+  return 0;
+}
+
+int scenario_failed() {
+  // a batch whose launch fails reports 0xff for each of its records (never 1), the others verify normally
+  Records r(300, 48);
+  OracleBackend be;
+  be.fail_launch_at = 1;
+  QueueOpts o;
+  o.max_batch = 100;
+  o.max_delay_us = 60000000;
+  o.max_msg_bytes = 48;
+  o.depth = 2;
+  BatchQueue<OracleBackend> q(be, o);
+  REQUIRE(q.start() == 0);
+  REQUIRE(q.submit(r.pk.data(), r.sig.data(), r.msg.data(), r.off.data(), r.n, nullptr) == 0);
+  std::vector<uint8_t> got(r.n, 0xee);
+  std::vector<uint64_t> order;
+  REQUIRE(drain(q, got, order, r.n, 20000000) == (long)r.n);
+  for (size_t i = 0; i < r.n; ++i) REQUIRE(i / 100 == 1 ? got[i] == 0xff : got[i] == r.want[i]);
+  const QueueStats s = q.stats();
+  printf("failed batches=%llu failed_batches=%llu\n", (unsigned long long)s.batches,
+         (unsigned long long)s.failed_batches);
+  REQUIRE(s.batches == 3 && s.failed_batches == 1);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   const char* s = argv[1];
@@ -248,5 +300,7 @@ int main(int argc, char** argv) {
   if (!strcmp(s, "deadline")) return scenario_deadline();
   if (!strcmp(s, "flush")) return scenario_flush();
   if (!strcmp(s, "drain")) return scenario_drain();
+  if (!strcmp(s, "startfail")) return scenario_startfail();
+  if (!strcmp(s, "failed")) return scenario_failed();
   return 2;
 }

@@ -91,8 +91,8 @@ def test_queue_matches_oracle_with_concurrent_producers(at2v_mod, oracle):
         st = q.stats()
     assert len(tickets) == n and np.array_equal(tickets, np.arange(n))  # every ticket, in order
     assert (ticket_of >= 0).all()
-    got = verdicts[ticket_of].astype(bool)
     assert not (verdicts == 0xFF).any()
+    got = verdicts[ticket_of] == 1
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     assert st["completed"] == n and st["batches"] >= n // 4096
 
@@ -136,9 +136,10 @@ def test_end_to_end_config1_pack_verify_apply(at2v_mod, verifier, oracle):
         t, v = _drain(q, n)
     assert np.array_equal(t, np.arange(first, first + n))
     want = oracle.verify_batch(rec["pk"], rec["sig"], rec["msg"], rec["off"])
-    assert np.array_equal(v.astype(bool), want) and (want == ~bad).all()
+    assert set(np.unique(v)) <= {0, 1}
+    assert np.array_equal(v == 1, want) and (want == ~bad).all()
     led = Ledger()
-    st = led.deliver(rec["pk"], rec["sequence"], rec["recipient"], rec["amount"], v.astype(bool))
+    st = led.deliver(rec["pk"], rec["sequence"], rec["recipient"], rec["amount"], v)  # queue bytes, fail closed
     assert st["rejected"] == bad.sum()
     # expected: per sender, sequences apply up to the first rejected one (a gap blocks the rest)
     bal = {}

@@ -205,9 +205,9 @@ def test_multi_gpu_context_if_available(at2v_mod, golden):
     v.close()
 
 
-def test_paired_chunks_adversarial(verifier, oracle):
-    """Enough records that every wave verifies chunk PAIRS (shared final inversion, Montgomery's trick):
-    > 2048 resident waves x 64 records. Adversarial mix, odd tail, compared record by record."""
+def test_many_chunks_per_wave_adversarial(verifier, oracle):
+    """Enough records that every resident wave (2048) takes several chunks from the chunk queue (262,181
+    records = 4097 chunks, the last one ragged), adversarial mix, compared record by record."""
     n = (1 << 18) + 37
     pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 2, 0, n, 64)
     want = oracle.verify_batch(pk, sig, msg, off)

@@ -20,6 +20,25 @@ def host_exe():
     return EXE
 
 
+@pytest.fixture(scope="module")
+def host_exe_asan():
+    exe = EXE + "_asan"
+    # -O0: the always-inline field code takes minutes to compile at -O1 under the sanitizers
+    subprocess.run(["g++", "-O0", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC, "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("half", [0, 1], ids=["full_length", "half_size"])
+def test_sanitized_host_build_of_device_core(host_exe_asan, half):
+    """the same code under AddressSanitizer + UBSan (signed overflow, shifts, bounds) over the edge and
+    adversarial fixtures"""
+    for name, limit in (("edge", 3000), ("adversarial", 800)):
+        out = subprocess.run([host_exe_asan, os.path.join(golden_io.GOLDEN_DIR, name + ".bin"), str(limit), str(half)],
+                             capture_output=True, text=True, timeout=900)
+        assert out.returncode == 0, out.stderr[-3000:]
+
+
 @pytest.mark.parametrize("half", [0, 1], ids=["full_length", "half_size"])
 @pytest.mark.parametrize("name", golden_io.SETS)
 def test_host_build_of_device_core_matches_golden(host_exe, name, half):

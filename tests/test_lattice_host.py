@@ -69,4 +69,24 @@ def test_corner_k(exe):
     ks += [(N8 // rng.randrange(2, 2**60)) % L for _ in range(100)]  # huge quotients deeper in the run
     pairs = [(k, rng.randrange(L)) for k in ks]
     res = run(exe, pairs)
-    check(pairs, res, slack=4)
+    worst = check(pairs, res, slack=4)
+    # the kernel's 64 radix-16 windows need bits <= 255 (verify_half fails a lane closed above that): the
+    # largest scalars come from tiny/huge first quotients, where the odd-c1 row is (k, 1) itself
+    assert worst <= 253, worst
+
+
+def test_bits_bound_near_lehmer_threshold(exe):
+    """k whose Euclid remainders straddle the stopping threshold ceil(sqrt(8l)) at every depth the
+    Lehmer rounds reach: the chosen vector must stay short (no candidate built from the huge row)"""
+    import math
+    rng = random.Random(9)
+    thr = math.isqrt(N8) + 1
+    ks = []
+    for _ in range(300):  # k = 8l / (thr + small) lands the first remainder next to the threshold
+        d = thr + rng.randrange(-2**20, 2**20)
+        ks.append((N8 // d) % L)
+        ks.append((N8 // d + rng.randrange(1, 2**16)) % L)
+    pairs = [(k, rng.randrange(L)) for k in ks]
+    res = run(exe, pairs)
+    worst = check(pairs, res, slack=4)
+    assert worst <= 253, worst

@@ -125,6 +125,36 @@ def test_rejected_verdicts_are_never_applied(led):
     assert led.balance(B) == INITIAL_BALANCE + 7
 
 
+def test_failed_batch_verdicts_apply_nothing(led):
+    """the queue reports 0xff for every record of a batch that failed on the device. Such
+    verdicts must never read as valid: delivery raises before anything reaches the ledger."""
+    from at2v.node import BatchFailedError
+    txs = [(A, 1, B, 10), (C, 1, B, 7), (A, 2, B, 1)]
+    for bad in (np.array([0xFF, 0xFF, 0xFF], np.uint8), np.array([1, 0xFF, 1], np.uint8)):
+        with pytest.raises(BatchFailedError):
+            deliver(led, txs, verdicts=bad)
+    for bad in (np.array([1, 2, 1], np.uint8), np.array([1, 0], np.uint8), np.array([0.0, 1.0, 1.0])):
+        with pytest.raises(ValueError):
+            deliver(led, txs, verdicts=bad)
+    assert led.pending() == 0 and led.balance(A) == INITIAL_BALANCE and led.balance(B) == INITIAL_BALANCE
+    assert led.last_sequence(A) == 0 and led.last_sequence(C) == 0
+    # plain 0/1 integers (queue bytes, Python lists) are per-record verdicts, never bitmap words
+    st = deliver(led, txs, verdicts=[0, 1, 0])
+    assert st["delivered"] == 1 and st["rejected"] == 2 and led.balance(B) == INITIAL_BALANCE + 7
+
+
+def test_bitmap_words_select_records(led):
+    n = 40
+    snd = np.repeat(np.frombuffer(C, np.uint8)[None], n, 0)
+    rcp = np.repeat(np.frombuffer(B, np.uint8)[None], n, 0)
+    words = np.array([0b101, 1 << 7], np.uint32)  # records 0, 2 and 39
+    st = led.deliver(snd, np.arange(1, n + 1, dtype=np.uint32), rcp, np.ones(n, np.uint64), words=words)
+    assert st["delivered"] == 3 and st["rejected"] == n - 3 and st["applied"] == 1  # seq 1 only: 3 and 40 wait
+    with pytest.raises(ValueError):
+        led.deliver(snd, np.arange(1, n + 1, dtype=np.uint32), rcp, np.ones(n, np.uint64),
+                    words=np.array([5, 0, 0], np.uint32))
+
+
 def test_out_of_order_sequences_apply_over_several_passes(led):
     """into_sorted_vec of BinaryHeap<Reverse<_>> walks the payloads in DESCENDING order: seq 3, 2, 1 take
     three passes to apply, and the loop stops after a pass that does not shrink the set"""

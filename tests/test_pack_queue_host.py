@@ -77,21 +77,36 @@ def test_pack_empty():
     assert out["pk"].shape == (0, 32) and list(out["off"]) == [0]
 
 
+# host builds of the queue core: plain, AddressSanitizer + UBSan, ThreadSanitizer (the product's threaded host
+# code; the oracle backend library itself is not instrumented)
+SANITIZE = {"plain": [], "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"],
+            "tsan": ["-fsanitize=thread", "-include", os.path.join(ROOT, "tests", "host", "tsan_compat.h")]}
+
+
 @pytest.fixture(scope="module")
 def queue_host():
-    exe = os.path.join(ROOT, "tests", "host", "queue_host")
     oracle_dir = os.path.join(ROOT, "oracle")
     subprocess.run(["make", "-s", "-C", oracle_dir, "all"], check=True)
-    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"),
-                    os.path.join(ROOT, "tests", "host", "queue_host.cpp"), "-L" + oracle_dir, "-loracle",
-                    "-Wl,-rpath," + oracle_dir, "-o", exe], check=True)
-    return exe
+    exes = {}
+    for kind, flags in SANITIZE.items():
+        exe = os.path.join(ROOT, "tests", "host", "queue_host" + ("" if kind == "plain" else "_" + kind))
+        subprocess.run(["g++", "-O1" if flags else "-O2", "-g", "-std=c++17", "-pthread", *flags,
+                        "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"),
+                        os.path.join(ROOT, "tests", "host", "queue_host.cpp"), "-L" + oracle_dir, "-loracle",
+                        "-Wl,-rpath," + oracle_dir, "-o", exe], check=True)
+        exes[kind] = exe
+    return exes
 
 
-@pytest.mark.parametrize("scenario", ["order", "size", "deadline", "flush", "drain"])
-def test_queue_core_on_host(queue_host, scenario):
+@pytest.mark.parametrize("build", list(SANITIZE))
+@pytest.mark.parametrize("scenario", ["order", "size", "deadline", "flush", "drain", "startfail", "failed"])
+def test_queue_core_on_host(queue_host, scenario, build):
     """order: 4 producer threads, random run lengths, verdicts map back through tickets (oracle backend);
     size: a full batch seals at max_batch; deadline: a partial batch seals at max_delay_us;
-    flush: explicit seal, oversized message rejected; drain: destroy completes everything submitted"""
-    out = subprocess.run([queue_host, scenario], capture_output=True, text=True, timeout=180)
-    assert out.returncode == 0, out.stdout + out.stderr
+    flush: explicit seal, oversized message rejected; drain: destroy completes everything submitted;
+    startfail: a start() that fails part-way frees every slot; failed: a batch whose launch fails
+    reports 0xff for its records and is counted in failed_batches. Each under ASan+UBSan and TSan too."""
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",
+               ASAN_OPTIONS="detect_leaks=1:halt_on_error=1")
+    out = subprocess.run([queue_host[build], scenario], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr[-4000:]

@@ -1,0 +1,140 @@
+"""CPU: the Rust FFI crate at2v-sys against include/at2v.h. No cargo/rustc in this image, so
+the check is textual: src/lib.rs's extern "C" block declares exactly the header's functions, with the same argument
+counts and the same integer widths / pointer depths per argument and return value; the #[repr(C)] structs have the
+header's fields in the header's order with the same widths; build.rs links libat2v the way the reference's build.rs
+(/root/reference/build.rs:1-3) hosts its codegen step."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "at2v.h")
+CRATE = os.path.join(ROOT, "at2v-sys")
+
+C_BASE = {"int": "i32", "at2v_policy": "i32", "size_t": "usize", "uint8_t": "u8", "uint32_t": "u32",
+          "uint64_t": "u64", "int32_t": "i32", "long": "long", "void": "void", "char": "char", "double": "f64",
+          "at2v_ctx": "ctx", "at2v_opts": "opts", "at2v_info": "info", "at2v_queue": "queue",
+          "at2v_queue_opts": "queue_opts", "at2v_queue_stats": "queue_stats", "at2v_ledger": "ledger",
+          "at2v_send_asset_request": "send_asset_request", "at2v_full_transaction": "full_transaction",
+          "at2v_apply_stats": "apply_stats"}
+R_BASE = {"c_int": "i32", "i32": "i32", "usize": "usize", "u8": "u8", "u32": "u32", "u64": "u64", "c_long": "long",
+          "c_void": "void", "c_char": "char", "f64": "f64", "At2vCtx": "ctx", "At2vOpts": "opts", "At2vInfo": "info",
+          "At2vQueue": "queue", "At2vQueueOpts": "queue_opts", "At2vQueueStats": "queue_stats",
+          "At2vLedger": "ledger", "At2vSendAssetRequest": "send_asset_request",
+          "At2vFullTransaction": "full_transaction", "At2vApplyStats": "apply_stats"}
+
+
+def c_type(decl: str) -> str:
+    """'const uint8_t* pk' / 'uint8_t out[AT2V_UNIQUE_ID_BYTES]' / 'size_t n' -> canonical 'ptr u8' etc."""
+    d = decl.replace("const", " ").strip()
+    depth = d.count("*") + (1 if "[" in d else 0)
+    d = re.sub(r"\[.*?\]", "", d).replace("*", " ")
+    words = d.split()
+    base = words[0] if len(words) == 1 or words[0] not in ("unsigned",) else words[1]
+    return "ptr " * depth + C_BASE[base]
+
+
+def r_type(t: str) -> str:
+    t = t.strip()
+    depth = 0
+    while t.startswith("*"):
+        depth += 1
+        t = re.sub(r"^\*(const|mut)\s+", "", t)
+    return "ptr " * depth + R_BASE[t]
+
+
+def header_functions():
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    txt = re.sub(r"#.*", "", txt)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(at2v_\w+)\s*\(([^;{]*?)\)\s*;", txt):
+        ret, name, args = m.group(1).strip(), m.group(2), m.group(3).strip()
+        ret = ret.split("\n")[-1].strip()
+        argl = [] if args in ("", "void") else [c_type(a) for a in args.split(",")]
+        out[name] = (c_type(ret + " x") if ret else "void", argl)
+    return out
+
+
+def crate_functions():
+    src = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    block = src[src.index('extern "C" {'):]
+    block = block[:block.index("\n}\n")]
+    out = {}
+    for m in re.finditer(r"pub fn (at2v_\w+)\((.*?)\)\s*(?:->\s*([^;]+))?;", block, flags=re.S):
+        name, args, ret = m.group(1), m.group(2), m.group(3)
+        argl = [r_type(a.split(":", 1)[1]) for a in args.split(",") if a.strip()]
+        out[name] = (r_type(ret) if ret else "void", argl)
+    return out
+
+
+def test_extern_block_matches_header():
+    h, r = header_functions(), crate_functions()
+    import at2v
+    assert sorted(h) == sorted(at2v.EXPORTED_SYMBOLS)
+    assert sorted(r) == sorted(h), set(r) ^ set(h)
+    for name in h:
+        assert r[name] == h[name], (name, "rust", r[name], "header", h[name])
+
+
+def header_structs():
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"typedef struct \{(.*?)\}\s*(at2v_\w+);", txt, flags=re.S):
+        fields = []
+        for line in m.group(1).split(";"):
+            line = " ".join(line.replace("const ", " ").split())
+            if not line:
+                continue
+            # "uint64_t submitted, completed" / "const uint8_t* sender" / "uint8_t sender[32]"
+            mm = re.match(r"(\w+)\s*(\**)\s*(.*)", line)
+            base, stars, rest = C_BASE[mm.group(1)], len(mm.group(2)), mm.group(3)
+            for nm in rest.split(","):
+                nm = nm.strip()
+                arr = re.search(r"\[(\d+)\]", nm)
+                star = stars + nm.count("*")
+                nm = re.sub(r"\[.*?\]|\*", "", nm).strip()
+                fields.append((nm, ("ptr " * star + base) + (f"[{arr.group(1)}]" if arr else "")))
+        out[m.group(2)] = fields
+    return out
+
+
+def crate_structs():
+    src = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    out = {}
+    for m in re.finditer(r"pub struct (At2v\w+) \{(.*?)\}", src, flags=re.S):
+        fields = []
+        for f in re.finditer(r"pub (\w+):\s*([^,]+),", m.group(2)):
+            t = f.group(2).strip()
+            arr = re.match(r"\[(\w+);\s*(\d+)\]", t)
+            fields.append((f.group(1), (r_type(arr.group(1)) + f"[{arr.group(2)}]") if arr else r_type(t)))
+        if fields:
+            out[m.group(1)] = fields
+    return out
+
+
+def test_repr_c_structs_match_header():
+    h, r = header_structs(), crate_structs()
+    pairs = {"at2v_opts": "At2vOpts", "at2v_info": "At2vInfo", "at2v_queue_opts": "At2vQueueOpts",
+             "at2v_queue_stats": "At2vQueueStats", "at2v_send_asset_request": "At2vSendAssetRequest",
+             "at2v_full_transaction": "At2vFullTransaction", "at2v_apply_stats": "At2vApplyStats"}
+    assert set(h) == set(pairs), set(h) ^ set(pairs)
+    for c, rs in pairs.items():
+        assert r[rs] == h[c], (c, r[rs], h[c])
+
+
+def test_constants_match_header():
+    txt = open(HEADER).read()
+    src = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    consts = dict(re.findall(r"\b(AT2V_[A-Z0-9_]+)\s*=\s*(-?\d+)", txt))
+    consts.update(re.findall(r"#define (AT2V_[A-Z0-9_]+) (\d+)", txt))
+    rust = dict(re.findall(r"pub const (AT2V_[A-Z0-9_]+): \w+ = (-?(?:0x)?[0-9a-f]+);", src))
+    for k, v in consts.items():
+        assert k in rust, k
+        assert int(rust[k], 0) == int(v), (k, rust[k], v)
+
+
+def test_build_script_links_libat2v():
+    b = open(os.path.join(CRATE, "build.rs")).read()
+    assert "cargo:rustc-link-lib=dylib=at2v" in b and "cargo:rustc-link-search=native=" in b
+    assert "AT2V_LIB_DIR" in b
+    toml = open(os.path.join(CRATE, "Cargo.toml")).read()
+    assert 'links = "at2v"' in toml and 'build = "build.rs"' in toml

@@ -34,14 +34,14 @@ sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
 def node_main(idx, inboxes, result_q, args, total):
     import numpy as np
 
-    from at2v.node import IngestQueue, Ledger, SendAssetRequest, pack_send_asset
+    from at2v.node import VERDICT_FAILED, IngestQueue, Ledger, SendAssetRequest, pack_send_asset, verdict_mask
 
     q = IngestQueue(device=0, max_batch=args.batch, max_delay_us=args.delay_us, max_msg_bytes=48, depth=3)
     led = Ledger()
     lock = threading.Lock()
     chunks = []  # submitted runs, ticket order: [first, pk, seq, rcp, amt, t_arrival]
     lat = []
-    stats = {"received": 0, "verified": 0, "rejected": 0, "applied": 0, "batches_delivered": 0}
+    stats = {"received": 0, "verified": 0, "rejected": 0, "applied": 0, "batches_delivered": 0, "failed": 0}
     done_ingest = threading.Event()
     t0 = time.perf_counter()
 
@@ -103,14 +103,18 @@ def node_main(idx, inboxes, result_q, args, total):
                     assert t[k] == first + used
                     sl = slice(used, used + take)
                     sel["pk"].append(c[1][sl]); sel["seq"].append(c[2][sl]); sel["rcp"].append(c[3][sl])
-                    sel["amt"].append(c[4][sl]); sel["ok"].append(v[k:k + take].astype(bool))
+                    sel["amt"].append(c[4][sl]); sel["ok"].append(v[k:k + take])
                     lat.extend([now - c[5]] * take)
                     c[6] += take
                     k += take
                     if c[6] == n_c:
                         chunks[ci] = None
                         ci += 1
-                okv = np.concatenate(sel["ok"])
+                raw = np.concatenate(sel["ok"])
+                if (raw == VERDICT_FAILED).any():  # a device failure: nothing of it is delivered (fail closed)
+                    stats["failed"] += int((raw == VERDICT_FAILED).sum())
+                    raw = np.where(raw == VERDICT_FAILED, 0, raw).astype(np.uint8)
+                okv = verdict_mask(raw, len(raw))
                 st = led.deliver(np.concatenate(sel["pk"]), np.concatenate(sel["seq"]), np.concatenate(sel["rcp"]),
                                  np.concatenate(sel["amt"]), okv, int((now - t0) * 1e6))
                 stats["verified"] += int(okv.sum())
@@ -242,7 +246,7 @@ def main():
            "ledgers_identical": same, "all_real_applied": all(r["applied"] == info["total"] - info["bad"] for r in res), "wall_s": wall, "offered_s": offered["offered_s"], "per_node": res}
     print(json.dumps(out), flush=True)
     ok = same and all(r["verified"] + r["rejected"] == info["total"] and r["rejected"] == info["bad"] and
-                      r["applied"] == info["total"] - info["bad"] and r["pending"] == 0 for r in res)
+                      r["applied"] == info["total"] - info["bad"] and r["pending"] == 0 and r["failed"] == 0 for r in res)
     return 0 if ok else 1
 
 
