@@ -13,8 +13,14 @@
 #include <hip/hip_runtime.h>
 
 #include "at2v_verify.h"
+#include "at2v_verify_fu.h"
+#include "at2v_fe_fu.h"
 
 namespace at2v {
+
+#ifndef AT2V_FIELD_FU
+#define AT2V_FIELD_FU 1  // 1: verify on the unsigned chained-carry field; 0: balanced signed field (§3)
+#endif
 
 #ifndef AT2V_VERIFY_WAVES_PER_SIMD
 #define AT2V_VERIFY_WAVES_PER_SIMD 2  // register budget: 512 / waves VGPR+AGPR per lane
@@ -75,7 +81,9 @@ struct DevTabA {
   int4* base;   // this lane's 1440-byte slot (global)
   int4* stage;  // this wave's 10 x 1 KiB LDS staging buffer for the prefetched entry
   int lane;
-  __device__ AT2V_INLINE void store(int e, const ge_cached& c) const {
+  template <class Cached>
+  __device__ AT2V_INLINE void store(int e, const Cached& c) const {
+    static_assert(sizeof(Cached) == 160, "cached point: 40 words");
     const int32_t* w = reinterpret_cast<const int32_t*>(&c);
 #pragma unroll
     for (int q = 0; q < 10; ++q) base[e * 10 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
@@ -100,7 +108,9 @@ struct DevTabA {
                                        (__attribute__((address_space(3))) void*)(stage + q * 64), 16,
                                        0, 0);
   }
-  __device__ AT2V_INLINE void load_prefetched(ge_cached& c) const {
+  template <class Cached>
+  __device__ AT2V_INLINE void load_prefetched(Cached& c) const {
+    static_assert(sizeof(Cached) == 160, "cached point: 40 words");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int32_t* w = reinterpret_cast<int32_t*>(&c);
 #pragma unroll
@@ -149,7 +159,9 @@ struct DevTabB {
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + e * 8 + q),
                                        (__attribute__((address_space(3))) void*)(stage + q * 64), 16, 0, 0);
   }
-  __device__ AT2V_INLINE void load_prefetched(ge_niels& n) const {
+  template <class Niels>
+  __device__ AT2V_INLINE void load_prefetched(Niels& n) const {
+    static_assert(sizeof(Niels) == 120, "Niels point: 30 words");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int32_t w[32];
 #pragma unroll
@@ -309,7 +321,11 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
       const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
       return __builtin_amdgcn_alignbit(hi, lo, sh);
     };
+#if AT2V_FIELD_FU
+    const int good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+#else
     const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+#endif
     const uint64_t mask = __ballot(good);
     uint32_t ticket = 0;
     if (lane == 0) {
@@ -627,6 +643,17 @@ __global__ __launch_bounds__(kBlock) void build_btab_kernel(int4* __restrict__ o
   ge_niels nj;
   ge_p2_to_niels(nj, P);
   int32_t w[32];
+#if AT2V_FIELD_FU && AT2V_VERIFY_HALF
+  {  // the verify kernel reads the tables on the unsigned field
+    gu_niels nu;
+    niels_fe_to_fu(nu, nj);
+    for (int k = 0; k < 10; ++k) {
+      nj.ypx.v[k] = (int32_t)nu.ypx.v[k];
+      nj.ymx.v[k] = (int32_t)nu.ymx.v[k];
+      nj.xy2d.v[k] = (int32_t)nu.xy2d.v[k];
+    }
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
     w[k] = nj.ypx.v[k];

@@ -1,0 +1,176 @@
+// at2v_verify_fu.h — per-lane half-size Ed25519 verify on the unsigned field (at2v_fu / at2v_gu).
+//
+// Same equation, checks and verdicts as verify_half (at2v_verify.h): accept <=> s < l, A decodes, R_bytes canonical and
+// decodes, and V = [c1]R + [c0]A - [t]B = 0 with (c0, c1) from lattice_reduce(k) and t = c1 s mod l. Replaces, per
+// record, drop::crypto::sign -> ed25519-dalek `PublicKey::verify` on every payload broadcast at
+// /root/reference/src/bin/server/rpc.rs:275-284. What changes is the arithmetic: unsigned limbs with the carry chained
+// through the MAD addend (tools/gen_fu.py), the A and R decodes as one interleaved pair of exponentiations, the two
+// per-lane tables built as interleaved pairs.
+//   TabP : store(e, gu_cached) / prefetch(e) / load_prefetched(gu_cached)   (per lane, e in 0..8)
+//   TabB : prefetch(e) / load_prefetched(gu_niels)                          (shared, e in 0..2^15)
+#pragma once
+#include "at2v_gu.h"
+#include "at2v_verify.h"
+
+namespace at2v {
+
+template <class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax, class Pace = NoPace>
+AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                       MsgWord msgword, int policy, TabP& ta, TabP& tr, const TabB0& tb0,
+                                       const TabB1& tb1, WaveMax wave_max, Pace&& pace = Pace()) {
+  // V1: s < l
+  int ok = sc_is_canonical(Sw);
+  if (policy == POLICY_LIBSODIUM_1_0_18) {
+    ok &= !enc_small_order(Rw);
+    ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
+  }
+  // V2: decode A and R together; R must be canonical (y < p, not x = 0 with the sign bit)
+  gu_p3 A, R;
+  {
+    int okd[2];
+    gu_frombytes_x2(A, Aw, R, Rw, okd);
+    ok &= okd[0] & okd[1];
+  }
+  ok &= enc_y_canonical(Rw);
+  ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
+  AT2V_PHASE(1);
+  pace.mark(10);
+  // V3: k = SHA-512(R || A || M) mod l
+  uint32_t k[8];
+  {
+    uint32_t pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = Rw[i];
+      pre[8 + i] = Aw[i];
+    }
+    uint64_t h[8];
+    sha512_prefixed<16>(h, pre, len, msgword);
+    uint32_t hw[16];
+    sha512_digest_words(hw, h);
+    sc_reduce512(k, hw);
+  }
+  AT2V_PHASE(5);
+  pace.mark(3);
+  HalfScalars hs;
+  lattice_reduce(hs, k);
+  AT2V_PHASE(7);
+  pace.mark(3);
+  uint32_t t[8];
+  sc_mul_signed(t, hs, Sw);
+  uint32_t c0d[8], c1d[8], td[8];
+  sc_recode4_hi8(c0d, hs.c0);
+  sc_recode4_hi8(c1d, hs.c1);
+  sc_recode16(td, t);
+  // 64 signed radix-16 digits hold values < 2^255 (the reduction keeps max(|c0|, |c1|) < 2^253); a lane
+  // that would need a 65th window fails closed
+  ok &= hs.bits <= 255;
+  const int nw_lane = ok ? hs.bits / 4 + 1 : 0;
+  int nw = wave_max(nw_lane);
+  nw = nw < 29 ? 29 : nw;  // B digits sit at windows 0, 4, ..., 28
+  AT2V_PHASE(2);
+  pace.mark(1);
+
+  // tables [j]A and [j](+-R), j = 0..8, built as one interleaved pair
+  if (hs.c1_neg) {
+    fu_neg(R.X, R.X, FU_KC);
+    fu_carry(R.X);
+    fu_neg(R.T, R.T, FU_KC);
+    fu_carry(R.T);
+  }
+  {
+    gu_cached ca1, cr1, cj;
+    gu_cached_identity(cj);
+    ta.store(0, cj);
+    tr.store(0, cj);
+    gu_p3_to_cached(ca1, A);
+    gu_p3_to_cached(cr1, R);
+    ta.store(1, ca1);
+    tr.store(1, cr1);
+    gu_p3 PA = A, PR = R;
+#pragma unroll 1
+    for (int j = 2; j <= 8; ++j) {
+      gu_p1p1 sa, sr;
+      gu_add(sa, PA, ca1);
+      gu_add(sr, PR, cr1);
+      gu_p1p1_to_p3(PA, sa);
+      gu_p1p1_to_p3(PR, sr);
+      gu_p3_to_cached(cj, PA);
+      ta.store(j, cj);
+      gu_p3_to_cached(cj, PR);
+      tr.store(j, cj);
+    }
+  }
+  AT2V_PHASE(3);
+  pace.mark(4);
+
+  // shared doubling chain over windows nw-1 .. 0:
+  //   acc = 16 acc + a_i A + r_i (+-R) + [4 | i, i < 32] (-t_{i/4} [2^(16 i/4)]B - t_{8+i/4} [2^(128+16 i/4)]B)
+  gu_p2 R2;
+  gu_p3 R3;
+  gu_p1p1 tt;
+  gu_cached ca;
+  gu_niels nb;
+  auto digit4 = [](const uint32_t d[8], int i) -> int { return (int)((sel8(d, i >> 3) >> (4 * (i & 7))) & 15) - 7; };
+  {
+    const int i = nw - 1;
+    const int da = digit4(c0d, i), dr = digit4(c1d, i);
+    ta.prefetch(da < 0 ? -da : da);
+    tr.prefetch(dr < 0 ? -dr : dr);
+    gu_p3_identity(R3);
+    ta.load_prefetched(ca);
+    gu_cached_cneg(ca, da < 0);
+    gu_add(tt, R3, ca);
+    gu_p1p1_to_p3(R3, tt);
+    tr.load_prefetched(ca);
+    gu_cached_cneg(ca, dr < 0);
+    gu_add(tt, R3, ca);
+    gu_p1p1_to_p2(R2, tt);
+  }
+  for (int i = nw - 2; i >= 0; --i) {
+    pace.window();
+    const int da = digit4(c0d, i), dr = digit4(c1d, i);
+    ta.prefetch(da < 0 ? -da : da);  // both land while the window's four doublings run
+    tr.prefetch(dr < 0 ? -dr : dr);
+    for (int r = 0; r < 3; ++r) {
+      gu_p2_dbl(tt, R2);
+      gu_p1p1_to_p2(R2, tt);
+    }
+    gu_p2_dbl(tt, R2);
+    gu_p1p1_to_p3(R3, tt);
+    pace.mid();
+    const bool bwin = (i & 3) == 0 && i < 32;
+    int e0 = 0, e1 = 0;
+    if (bwin) {  // -t digits j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B)
+      e0 = (1 << 15) - (int)((sel8(td, i >> 3) >> (16 * ((i >> 2) & 1))) & 0xffff);
+      e1 = (1 << 15) - (int)((sel8(td, 4 + (i >> 3)) >> (16 * ((i >> 2) & 1))) & 0xffff);
+    }
+    ta.load_prefetched(ca);
+    if (bwin) tb0.prefetch(e0 < 0 ? -e0 : e0);  // into A's stage, now consumed
+    gu_cached_cneg(ca, da < 0);
+    gu_add(tt, R3, ca);
+    gu_p1p1_to_p3(R3, tt);
+    tr.load_prefetched(ca);
+    if (bwin) tb1.prefetch(e1 < 0 ? -e1 : e1);  // into R's stage
+    gu_cached_cneg(ca, dr < 0);
+    gu_add(tt, R3, ca);
+    if (bwin) {
+      gu_p1p1_to_p3(R3, tt);
+      tb0.load_prefetched(nb);
+      gu_niels_cneg(nb, e0 < 0);
+      gu_madd(tt, R3, nb);
+      gu_p1p1_to_p3(R3, tt);
+      tb1.load_prefetched(nb);
+      gu_niels_cneg(nb, e1 < 0);
+      gu_madd(tt, R3, nb);
+    }
+    gu_p1p1_to_p2(R2, tt);
+  }
+  AT2V_PHASE(4);
+  // V == identity: X = 0 and Y = Z
+  fu d;
+  fu_sub(d, R2.Y, R2.Z, FU_KC);
+  return ok & fu_iszero(R2.X) & fu_iszero(d);
+}
+
+}  // namespace at2v

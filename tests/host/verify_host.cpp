@@ -7,6 +7,8 @@
 #include <vector>
 
 #include "at2v_verify.h"
+#include "at2v_verify_fu.h"
+#include "at2v_fe_fu.h"
 
 using namespace at2v;
 
@@ -77,6 +79,26 @@ struct HostTabB16Hi {
   void load_prefetched(ge_niels& n) const { n = t[pending]; }
 };
 
+struct HostTabAFu {
+  gu_cached e[9];
+  int pending = 0;
+  void store(int i, const gu_cached& c) { e[i] = c; }
+  void prefetch(int i) { pending = i; }
+  void load_prefetched(gu_cached& c) const { c = e[pending]; }
+};
+// unsigned-field copy of a signed-field fixed-base table
+template <class T>
+struct HostTabBFu {
+  std::vector<gu_niels> t;
+  mutable int pending = 0;
+  explicit HostTabBFu(const T& src) {
+    t.resize(src.t.size());
+    for (size_t j = 0; j < t.size(); ++j) niels_fe_to_fu(t[j], src.t[j]);
+  }
+  void prefetch(int e) const { pending = e; }
+  void load_prefetched(gu_niels& n) const { n = t[pending]; }
+};
+
 static void words(uint32_t w[8], const uint8_t* b) {
   for (int i = 0; i < 8; ++i) w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
@@ -95,7 +117,7 @@ int main(int argc, char** argv) {
   (void)ok;
   size_t bad_d = 0, bad_s = 0;
   int limit = argc > 2 ? atoi(argv[2]) : (int)n;
-  const int half = argc > 3 ? atoi(argv[3]) : 0;  // 1: the half-size equation (verify_half)
+  const int half = argc > 3 ? atoi(argv[3]) : 0;  // 1: the half-size equation (verify_half); 2: on the unsigned field
   for (size_t i = 0; i < n && (int)i < limit; ++i) {
     uint32_t R[8], A[8], S[8];
     words(R, &sig[64 * i]);
@@ -111,7 +133,15 @@ int main(int argc, char** argv) {
     static HostTabB16 tb;
     HostTabA ta, tr;
     int d, s;
-    if (half) {
+    if (half == 2) {
+      static HostTabB16Hi tb1s;
+      static HostTabBFu<HostTabB16> fb0(tb);
+      static HostTabBFu<HostTabB16Hi> fb1(tb1s);
+      HostTabAFu fa, fr;
+      auto one = [](int v) { return v; };
+      d = verify_half_fu(R, A, S, len, mw, POLICY_DALEK_V1, fa, fr, fb0, fb1, one);
+      s = verify_half_fu(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, fa, fr, fb0, fb1, one);
+    } else if (half) {
       static HostTabB16Hi tb1;
       auto one = [](int v) { return v; };
       d = verify_half(R, A, S, len, mw, POLICY_DALEK_V1, ta, tr, tb, tb1, one);

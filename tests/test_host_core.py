@@ -29,7 +29,7 @@ def host_exe_asan():
     return exe
 
 
-@pytest.mark.parametrize("half", [0, 1], ids=["full_length", "half_size"])
+@pytest.mark.parametrize("half", [0, 1, 2], ids=["full_length", "half_size", "half_size_unsigned_field"])
 def test_sanitized_host_build_of_device_core(host_exe_asan, half):
     """the same code under AddressSanitizer + UBSan (signed overflow, shifts, bounds) over the edge and
     adversarial fixtures"""
@@ -39,16 +39,36 @@ def test_sanitized_host_build_of_device_core(host_exe_asan, half):
         assert out.returncode == 0, out.stderr[-3000:]
 
 
-@pytest.mark.parametrize("half", [0, 1], ids=["full_length", "half_size"])
+@pytest.mark.parametrize("half", [0, 1, 2], ids=["full_length", "half_size", "half_size_unsigned_field"])
 @pytest.mark.parametrize("name", golden_io.SETS)
 def test_host_build_of_device_core_matches_golden(host_exe, name, half):
-    """both verify equations the kernel can be built with: the full-length ladder (verify_core) and the
-    half-size lattice form (verify_half, the default), against OpenSSL/libsodium-derived verdicts"""
+    """every verify form the kernel can be built with: the full-length ladder (verify_core), the half-size lattice
+    form on the signed field (verify_half) and on the unsigned chained-carry field (verify_half_fu, the default),
+    against OpenSSL/libsodium-derived verdicts"""
     out = subprocess.run([host_exe, os.path.join(golden_io.GOLDEN_DIR, name + ".bin"), "1000000", str(half)],
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     n, bad_d, bad_s = map(int, out.stdout.split())
     assert bad_d == 0 and bad_s == 0 and n > 0
+
+
+def test_unsigned_field_bounds_at_class_extremes():
+    """the unsigned-field group law (at2v_gu.h) on maximal-limb inputs with every operand and column checked
+    (-DAT2V_FU_CHECK), plus value checks of the formulas from such representatives"""
+    exe = os.path.join(ROOT, "tests", "host", "fu_bounds_host")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-DAT2V_FU_CHECK", "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "host", "fu_bounds_host.cpp"), "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stderr[-2000:]
+
+
+def test_unsigned_field_generator_is_current():
+    """at2v_fu_gen.h must be what tools/gen_fu.py (bound proof + group-law model) emits."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "g.h")
+        subprocess.run(["python3", os.path.join(ROOT, "tools", "gen_fu.py"), p], check=True, capture_output=True)
+        assert open(p).read() == open(os.path.join(ROOT, "at2-node_amd", "csrc", "at2v_fu_gen.h")).read()
 
 
 def test_field_bounds_generator_is_current():
