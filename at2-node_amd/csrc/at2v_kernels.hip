@@ -313,7 +313,14 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     load8(Aw, pk + (size_t)ii * 32);
     const uint32_t o0 = off[ii];
     const uint32_t len = off[ii + 1] - o0;
+    // message words: a wave whose messages all end >= 8 bytes before the buffer end reads two aligned words and
+    // funnel-shifts them (no per-lane branch); otherwise every byte is bounds-checked (the last records of a batch)
+    const int msg_fast =
+        __builtin_amdgcn_readfirstlane(__all((uint64_t)o0 + len + 8 <= (uint64_t)msg_total) ? 1 : 0);
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (o0 >> 2);
+    const uint32_t msh = (o0 & 3u) * 8;
     auto msgword = [&](uint32_t j) -> uint32_t {
+      if (msg_fast) return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh);
       const uint32_t a = o0 + 4 * j;
       const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
       const uint32_t lo = load_u32_guarded(msg, a0, msg_total);

@@ -1,9 +1,9 @@
 // at2v_sha512.h — SHA-512 (FIPS 180-4), one message per lane, for k = H(R || A || M) (SURVEY A V3)
 // and for the deterministic record generator / signer kernels.
 //
-// 64-bit words are emulated on the 32-bit VALU by the compiler (rotations -> v_alignbit_b32 pairs,
-// additions -> v_add_co/v_addc). The 80 rounds run as 5 rolled iterations of a 16-round unrolled
-// body whose message schedule lives in a 16-entry circular register window.
+// 64-bit words on the 32-bit VALU: rotations as v_alignbit_b32 pairs, additions as v_lshl_add_u64. Rounds take the
+// working variables in rotated order (no moves); the first 16 rounds are peeled, the other 64 run as a rolled loop of
+// a 16-round body whose message schedule lives in a 16-entry circular register window.
 #pragma once
 #include "at2v_fe_base.h"
 
@@ -27,7 +27,23 @@ AT2V_CONST_ARR uint64_t SHA512_K[80] = {
     0x113f9804bef90daeULL, 0x1b710b35131c471bULL, 0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL,
     0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-AT2V_HD AT2V_INLINE uint64_t sha_ror(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+AT2V_HD AT2V_INLINE uint64_t sha_ror(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // two v_alignbit_b32 (a 64-bit shift pair + OR would be four instructions)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rlo, rhi;
+  if (n < 32) {
+    rlo = __builtin_amdgcn_alignbit(hi, lo, n);
+    rhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rhi << 32) | rlo;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 AT2V_HD AT2V_INLINE uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -38,28 +54,47 @@ AT2V_HD AT2V_INLINE void sha512_init(uint64_t h[8]) {
   h[6] = 0x1f83d9abfb41bd6bULL; h[7] = 0x5be0cd19137e2179ULL;
 }
 
-// one compression; w[16] = the block as big-endian 64-bit words (clobbered)
-AT2V_HD AT2V_INLINE void sha512_compress(uint64_t h[8], uint64_t w[16]) {
-  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-  for (int r = 0; r < 80; r += 16) {
+// one round with the working variables passed in rotated order (no register moves between rounds)
+AT2V_HD AT2V_INLINE void sha512_round(uint64_t a, uint64_t b, uint64_t c, uint64_t& d, uint64_t e, uint64_t f,
+                                      uint64_t g, uint64_t& h, uint64_t kw) {
+  const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t t1 = h + S1 + ch + kw;
+  const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
+  const uint64_t mj = (a & b) ^ (c & (a ^ b));
+  d += t1;
+  h = t1 + S0 + mj;
+}
+
+// 16 rounds r0 .. r0+15; SCHED: extend the message schedule in the 16-word circular window first
+template <bool SCHED>
+AT2V_HD AT2V_INLINE void sha512_rounds16(uint64_t s[8], uint64_t w[16], int r0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (r > 0) {
-        const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-        const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
-        w[i] += s0 + w[(i + 9) & 15] + s1;
-      }
-      const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t t1 = hh + S1 + ch + SHA512_K[r + i] + w[i];
-      const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
-      const uint64_t mj = (a & b) ^ (c & (a ^ b));
-      const uint64_t t2 = S0 + mj;
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  for (int i = 0; i < 16; ++i) {
+    if (SCHED) {
+      const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
+      w[i] += s0 + w[(i + 9) & 15] + s1;
     }
+    const uint64_t kw = SHA512_K[r0 + i] + w[i];
+    // working variable j of round i is s[(j - i) mod 8] (a = s[0] in round 0)
+    sha512_round(s[(8 - i % 8) % 8], s[(9 - i % 8) % 8], s[(10 - i % 8) % 8], s[(11 - i % 8) % 8],
+                 s[(12 - i % 8) % 8], s[(13 - i % 8) % 8], s[(14 - i % 8) % 8], s[(15 - i % 8) % 8], kw);
   }
-  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// one compression; w[16] = the block as big-endian 64-bit words (clobbered). The first 16 rounds use the block as
+// is; the other 64 run as a rolled loop of a 16-round body (a multiple of 8 rounds: the rotated names line up).
+AT2V_HD AT2V_INLINE void sha512_compress(uint64_t h[8], uint64_t w[16]) {
+  uint64_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = h[i];
+  sha512_rounds16<false>(s, w, 0);
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) sha512_rounds16<true>(s, w, r);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] += s[i];
 }
 
 // digest -> 16 little-endian 32-bit words of the 64-byte output (as bytes: big-endian h[0..7])
@@ -73,7 +108,8 @@ AT2V_HD AT2V_INLINE void sha512_digest_words(uint32_t out[16], const uint64_t h[
 
 // SHA-512 of (prefix || M) where prefix is np 32-byte-word chunks given as LE words (np*8 words,
 // np in {0,1,2}) and M is read through `msgword(j)` = the j-th little-endian 32-bit word of M
-// (bytes 4j..4j+3; bytes past len may be garbage — they are masked here). len < 2^32.
+// (bytes 4j..4j+3; bytes past len may be garbage — they are masked here). msgword is called for every word of every
+// block, with j clamped to len/4. len < 2^32.
 template <int NPW, class MsgWord>
 AT2V_HD AT2V_INLINE void sha512_prefixed(uint64_t h[8], const uint32_t* prefix, uint32_t len, MsgWord msgword) {
   sha512_init(h);
@@ -93,8 +129,8 @@ AT2V_HD AT2V_INLINE void sha512_prefixed(uint64_t h[8], const uint32_t* prefix, 
           le = prefix[(2 * t + half) < NPW ? (2 * t + half) : 0];
         } else {
           const uint32_t mo = pos - 4 * NPW;                 // message byte offset
-          uint32_t v = 0;
-          if (mo < len) v = msgword(mo >> 2);
+          // every lane reads a word (bytes past len are masked below): no divergent branch per word
+          uint32_t v = msgword((mo < len ? mo : len) >> 2);
           const uint32_t nvalid = mo >= len ? 0u : (len - mo >= 4 ? 4u : len - mo);
           if (nvalid < 4) {
             v = nvalid ? (v & ((1u << (8 * nvalid)) - 1)) : 0u;
