@@ -53,7 +53,12 @@ class VerifyError(Exception):
 
 
 class _Opts(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int)]
+    _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int),
+                ("small_batch_max", ctypes.c_uint32)]
+
+
+SMALL_BATCH_DEFAULT = 32768     # include/at2v.h AT2V_SMALL_BATCH_DEFAULT
+SMALL_BATCH_OFF = 0xFFFFFFFF    # include/at2v.h AT2V_SMALL_BATCH_OFF: never use the low-latency kernel
 
 
 class _Info(ctypes.Structure):
@@ -160,10 +165,12 @@ def pack_records(pks: Sequence[bytes], sigs: Sequence[bytes], msgs: Sequence[byt
 class BatchVerifier:
     """Owns an at2v context (one or more gfx950 devices)."""
 
-    def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek"):
+    def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek", small_batch_max: int = 0):
+        """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
+        0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel."""
         self._lib = load_library()
         self.policy = _POLICIES[policy]
-        opts = _Opts(device, num_gpus, self.policy)
+        opts = _Opts(device, num_gpus, self.policy, small_batch_max)
         h = ctypes.c_void_p()
         _check(self._lib.at2v_create(ctypes.byref(opts), ctypes.byref(h)), "at2v_create")
         self._h = h

@@ -64,9 +64,13 @@ class AccountError(Exception):
         self.code = code
 
 
+QUEUE_EAGER = 1  # include/at2v.h AT2V_QUEUE_EAGER: also seal whenever no batch is in flight
+
+
 class _QueueOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("policy", ctypes.c_int), ("max_batch", ctypes.c_uint32),
-                ("max_delay_us", ctypes.c_uint32), ("max_msg_bytes", ctypes.c_uint32), ("depth", ctypes.c_uint32)]
+                ("max_delay_us", ctypes.c_uint32), ("max_msg_bytes", ctypes.c_uint32), ("depth", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
 
 
 class _QueueStats(ctypes.Structure):
@@ -137,10 +141,11 @@ class IngestQueue:
     """GPU-backed batching queue: submit records, poll (ticket, verdict) in submission order."""
 
     def __init__(self, device: int = 0, policy="dalek", max_batch: int = 65536, max_delay_us: int = 1000,
-                 max_msg_bytes: int = 256, depth: int = 3):
+                 max_msg_bytes: int = 256, depth: int = 3, eager: bool = False):
         from . import _POLICIES
         self._lib = _lib()
-        o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth)
+        o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth,
+                       QUEUE_EAGER if eager else 0)
         h = ctypes.c_void_p()
         _chk(self._lib.at2v_queue_create(ctypes.byref(o), ctypes.byref(h)), "at2v_queue_create")
         self._h = h

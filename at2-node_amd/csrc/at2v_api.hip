@@ -27,7 +27,7 @@
 namespace at2v {
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, hipStream_t stream);
+                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream);
 size_t btab_bytes();
 hipError_t launch_build_btab(int4* out, hipStream_t stream);
 hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint8_t* pk, uint8_t* sig,
@@ -78,6 +78,7 @@ struct Shard {
 
 struct at2v_ctx {
   at2v_policy policy = AT2V_POLICY_DALEK_V1;
+  uint32_t pair_max = AT2V_SMALL_BATCH_DEFAULT;  // launches of <= this many records: low-latency kernel
   std::vector<Shard> shards;
   ncclComm_t comm = nullptr;  // at2v_comm_init_rank (one rank per process, the context's first device)
   int rank = 0, world = 1;
@@ -131,7 +132,7 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   if (e == hipSuccess) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
   if (e == hipSuccess)
     e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch.p,
-                            (const int4*)s.btab.p, s.grid, stream);
+                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream);
   if (e == hipSuccess) e = hipEventRecord(s.scratch_free, stream);
   return e;
 }
@@ -151,7 +152,7 @@ extern "C" {
 int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
-  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1};
+  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1, 0};
   if (opts) o = *opts;
   if (o.num_gpus <= 0) o.num_gpus = 1;
   if (o.policy != AT2V_POLICY_DALEK_V1 && o.policy != AT2V_POLICY_LIBSODIUM_1_0_18) return AT2V_E_INVALID;
@@ -161,6 +162,8 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   at2v_ctx* c = new (std::nothrow) at2v_ctx;
   if (!c) return AT2V_E_OOM;
   c->policy = o.policy;
+  c->pair_max = o.small_batch_max == 0 ? AT2V_SMALL_BATCH_DEFAULT
+                : o.small_batch_max == AT2V_SMALL_BATCH_OFF ? 0u : o.small_batch_max;
   c->shards.resize((size_t)o.num_gpus);
   int prev = 0;
   (void)hipGetDevice(&prev);

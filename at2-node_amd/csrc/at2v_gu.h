@@ -185,4 +185,43 @@ AT2V_HD AT2V_INLINE void gu_frombytes_x2(gu_p3& h0, const uint32_t s0[8], gu_p3&
   fu_mulc_x2(h0.T, h0.X, h0.Y, h1.T, h1.X, h1.Y);
 }
 
+// one encoding (the low-latency kernel decodes A and R on two lanes, one each): same steps as gu_frombytes_x2
+AT2V_HD AT2V_INLINE int gu_frombytes(gu_p3& h, const uint32_t s[8]) {
+  fu u, v, v3, t;
+  fu_frombytes(h.Y, s);
+  fu_1(h.Z);
+  fu_sqc(u, h.Y);
+  fu_mulc(v, u, FU_D);
+  fu_add(u, u, FU_PM1);  // u = y^2 - 1
+  v.v[0] += 1;           // v = d y^2 + 1
+  fu_sq(v3, v);
+  fu_mul(v3, v3, v);     // v^3
+  fu_sqc(t, v3);
+  fu_mul(t, t, v);       // v^7
+  fu_mul(t, u, t);       // u v^7
+  fu_pow22523(t, t);     // (u v^7)^((p-5)/8)
+  fu_mulc(t, t, v3);
+  fu_mul(h.X, u, t);     // r = u v^3 (u v^7)^((p-5)/8)
+  fu vxx, ui, xi, chk;
+  fu_sqc(vxx, h.X);
+  fu_mul(vxx, v, vxx);   // v r^2
+  fu_mul(ui, u, FU_SQRTM1);
+  fu_mulc(xi, h.X, FU_SQRTM1);
+  fu_sub(chk, vxx, u, FU_K2C);
+  const int correct = fu_iszero(chk);
+  fu_add(chk, vxx, u);
+  const int flipped = fu_iszero(chk);
+  fu_add(chk, vxx, ui);  // v r^2 == -u*i  <=>  v r^2 + u i == 0
+  const int flipped_i = fu_iszero(chk);
+  fu_select(h.X, h.X, xi, flipped | flipped_i);
+  fu neg;
+  fu_neg(neg, h.X, FU_KC);
+  fu_select(h.X, h.X, neg, fu_isnegative(h.X));  // non-negative root
+  fu_neg(neg, h.X, FU_KC);
+  fu_select(h.X, h.X, neg, (int)(s[7] >> 31));   // apply the encoded sign
+  fu_carry(h.X);
+  fu_mulc(h.T, h.X, h.Y);
+  return correct | flipped;
+}
+
 }  // namespace at2v

@@ -127,13 +127,15 @@ extern "C" {
 int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
-  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0};
+  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0};
   if (opts) o = *opts;
   at2v::QueueOpts qo;
   if (o.max_batch) qo.max_batch = o.max_batch;
   if (o.max_delay_us) qo.max_delay_us = o.max_delay_us;
   if (o.max_msg_bytes) qo.max_msg_bytes = o.max_msg_bytes;
   if (o.depth) qo.depth = (int)o.depth;
+  qo.eager = (o.flags & AT2V_QUEUE_EAGER) != 0;
+  if (o.flags & ~AT2V_QUEUE_EAGER) return AT2V_E_INVALID;
   if (qo.depth < 2 || qo.max_batch >= (1u << 31) || (uint64_t)qo.max_batch * qo.max_msg_bytes >= (1ull << 32))
     return AT2V_E_INVALID;
   at2v_queue* q = new (std::nothrow) at2v_queue;

@@ -359,6 +359,74 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     AT2V_PHASE(6);
   }
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Low-latency verify for small launches: two lanes per record (lane 2r: A side, lane 2r+1: R side,
+// verify_pair_part), 32 records per wave, one wave per SIMD (4-wave blocks, 80 KiB LDS). Each lane decodes one point,
+// builds one table and does one addition per window; the partner's cached point comes across by __shfl_xor and both
+// lanes evaluate V = P0 + P1 (verify_pair_combine). Chunks c = 32-record groups, grid-strided.
+constexpr int kPairBlock = 256;
+constexpr int kPairWaves = kPairBlock / 64;
+__global__ __launch_bounds__(kPairBlock, 1) void verify_pair_kernel(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab) {
+  __shared__ int4 pstage[kPairWaves * 10 * 64];
+  __shared__ int4 bstage[kPairWaves * 10 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const int side = lane & 1;
+  const uint32_t wave = blockIdx.x * kPairWaves + wib;
+  const uint32_t nwaves = gridDim.x * kPairWaves;
+  const uint32_t nchunks = (n + 31) / 32;
+  int4* slot = scratch + ((size_t)wave * 64 + lane) * kTabAGranules;
+  DevTabA tp{slot, pstage + wib * 640, lane};
+  const DevTabB tb{btab + (size_t)side * kBtabEntries * 8, bstage + wib * 640, lane};
+  auto wmax = [](int v) { return wave_max_i32(v); };
+  for (uint32_t c = wave; c < nchunks; c += nwaves) {
+    const uint32_t i = c * 32 + (lane >> 1);
+    const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
+    uint32_t Rw[8], Sw[8], Aw[8];
+    load8(Rw, sig + (size_t)ii * 64);
+    load8(Sw, sig + (size_t)ii * 64 + 32);
+    load8(Aw, pk + (size_t)ii * 32);
+    const uint32_t o0 = off[ii];
+    const uint32_t len = off[ii + 1] - o0;
+    const int msg_fast =
+        __builtin_amdgcn_readfirstlane(__all((uint64_t)o0 + len + 8 <= (uint64_t)msg_total) ? 1 : 0);
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (o0 >> 2);
+    const uint32_t msh = (o0 & 3u) * 8;
+    auto msgword = [&](uint32_t j) -> uint32_t {
+      if (msg_fast) return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh);
+      const uint32_t a = o0 + 4 * j;
+      const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+      const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+      if (sh == 0) return lo;
+      const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+      return __builtin_amdgcn_alignbit(hi, lo, sh);
+    };
+    gu_p3 Pm;
+    int ok = verify_pair_part(side, Rw, Aw, Sw, len, msgword, policy, tp, tb, wmax, Pm);
+    gu_cached cm, cp;
+    gu_p3_to_cached(cm, Pm);
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(&cm);
+    uint32_t* pw = reinterpret_cast<uint32_t*>(&cp);
+#pragma unroll
+    for (int q = 0; q < 40; ++q) pw[q] = (uint32_t)__shfl_xor((int)cw[q], 1);
+    ok &= __shfl_xor(ok, 1);
+    const int good = ok & verify_pair_combine(Pm, cp) & (i < n);
+    const uint64_t mask = __ballot(good);
+    if (lane == 0) {  // record r's verdict is lane 2r's bit: compress the even bits of the ballot
+      uint64_t x = mask & 0x5555555555555555ull;
+      x = (x | (x >> 1)) & 0x3333333333333333ull;
+      x = (x | (x >> 2)) & 0x0f0f0f0f0f0f0f0full;
+      x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
+      x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
+      x = (x | (x >> 16)) & 0x00000000ffffffffull;
+      verdicts[c] = (uint32_t)x;
+    }
+  }
+}
 #else
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -709,8 +777,20 @@ hipError_t launch_build_btab(int4* out, hipStream_t stream) {
 
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, hipStream_t stream) {
+                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream) {
   if (n == 0) return hipSuccess;
+#if AT2V_VERIFY_HALF && AT2V_FIELD_FU
+  if (n <= pair_max) {
+    // one wave (32 records) per SIMD: 4-wave blocks; the context's scratch holds grid x 8 waves of (larger) slots
+    const uint32_t nchunks = (n + 31) / 32;
+    const uint32_t cap_blocks = (uint32_t)grid * kWavesPerBlock / kPairWaves;
+    uint32_t g = (nchunks + kPairWaves - 1) / kPairWaves;
+    g = g < cap_blocks ? g : cap_blocks;
+    hipLaunchKernelGGL(verify_pair_kernel, dim3(g), dim3(kPairBlock), 0, stream, pk, sig, msg, msg_total, off, n,
+                       policy, verdicts, scratch, btab);
+    return hipGetLastError();
+  }
+#endif
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t need_blocks = (nchunks + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);  // half-filled blocks
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);

@@ -6,7 +6,9 @@
 // deliver() (rpc.rs:156-173). This queue is the MI355X-side replacement of that per-payload step:
 //   * producers submit records (A, R||S, M) and get monotonically increasing tickets;
 //   * a launcher thread seals the filling batch when it holds `max_batch` records, when its oldest
-//     record is `max_delay_us` old, or on flush(), and starts an asynchronous verify of it;
+//     record is `max_delay_us` old, or on flush(), and starts an asynchronous verify of it; in eager
+//     mode it also seals as soon as no batch is in flight (latency mode: a lone record is launched at
+//     once, and records arriving during a verify form the next batch, so batch size follows the load);
 //   * a completer thread waits for batches in launch order and publishes (ticket, verdict) in ticket
 //     order, so verdicts map back to payloads without any per-record bookkeeping by the caller;
 //   * `depth` batch slots: one filling while up to depth-1 are in flight (copy/compute overlap).
@@ -37,6 +39,7 @@ struct QueueOpts {
   uint32_t max_delay_us = 1000;
   size_t max_msg_bytes = 256;  // average message bytes budgeted per record (slot msg capacity = max_batch x this)
   int depth = 3;               // slots: 1 filling + up to depth-1 in flight
+  bool eager = false;          // also seal whenever the device is idle (no batch in flight)
 };
 
 struct QueueSlot {
@@ -239,7 +242,8 @@ class BatchQueue {
     std::unique_lock<std::mutex> lk(m_);
     while (true) {
       if (fill_ && fill_->n) {
-        if (flush_req_ || now_us() >= fill_->t_first + o_.max_delay_us) seal_locked();
+        const bool idle = inflight_.empty() && ready_.empty() && !launching_;
+        if (flush_req_ || now_us() >= fill_->t_first + o_.max_delay_us || (o_.eager && idle)) seal_locked();
       }
       if (flush_req_ && (!fill_ || fill_->n == 0)) flush_req_ = false;
       if (!ready_.empty()) {
@@ -294,6 +298,7 @@ class BatchQueue {
       free_.push_back(s);
       cv_free_.notify_all();
       cv_done_.notify_all();
+      if (o_.eager) cv_launch_.notify_all();  // the device went idle: seal what is filling
       if ((!fill_ || fill_->n == 0) && ready_.empty() && !launching_ && inflight_.empty()) cv_idle_.notify_all();
     }
   }

@@ -293,7 +293,7 @@ AT2V_HD AT2V_INLINE int verify_half(const uint32_t Rw[8], const uint32_t Aw[8], 
   ok &= hs.bits <= 255;
   const int nw_lane = ok ? hs.bits / 4 + 1 : 0;  // windows for values < 2^(4 nw - 1); <= 64
   int nw = wave_max(nw_lane);
-  nw = nw < 29 ? 29 : nw;  // B digits sit at windows 0, 4, ..., 28
+  nw = nw < 30 ? 30 : nw;  // B digits sit at windows 0, 4, ..., 28: the top window (no B digit) must lie above them
   AT2V_PHASE(2);
   pace.mark(1);
 

@@ -67,7 +67,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   ok &= hs.bits <= 255;
   const int nw_lane = ok ? hs.bits / 4 + 1 : 0;
   int nw = wave_max(nw_lane);
-  nw = nw < 29 ? 29 : nw;  // B digits sit at windows 0, 4, ..., 28
+  nw = nw < 30 ? 30 : nw;  // B digits sit at windows 0, 4, ..., 28: the top window (no B digit) must lie above them
   AT2V_PHASE(2);
   pace.mark(1);
 
@@ -171,6 +171,141 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   fu d;
   fu_sub(d, R2.Y, R2.Z, FU_KC);
   return ok & fu_iszero(R2.X) & fu_iszero(d);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Two lanes per signature (the low-latency kernel). Side 0 owns A, side 1 owns R: each lane decodes
+// one point, builds one table, and runs its half of the shared-window chain,
+//   side 0: P0 = [c0]A - [t_lo]B          side 1: P1 = [c1]R - [t_hi 2^128]B   (t = t_lo + 2^128 t_hi),
+// so a lane does four doublings and one addition per window instead of two additions, and one of the two
+// fixed-base additions. V = P0 + P1 is then formed from the partner's cached point (verify_pair_combine). The
+// SHA-512 and the lattice reduction run on both lanes (same code, no divergence). Returns this side's checks:
+// side 0 V1, the policy pre-checks and A's decode; side 1 R's decode and canonicity. The signature is valid iff both
+// sides' checks pass and V is the identity.
+//   TabP : this lane's table of its point;  TabB : this lane's fixed-base table ([j]B on side 0, [j 2^128]B on side 1)
+template <class TabP, class TabB, class MsgWord, class WaveMax>
+AT2V_HD AT2V_INLINE int verify_pair_part(int side, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
+                                         uint32_t len, MsgWord msgword, int policy, TabP& tp, const TabB& tb,
+                                         WaveMax wave_max, gu_p3& out) {
+  int ok;
+  gu_p3 P;
+  if (side == 0) {
+    ok = sc_is_canonical(Sw);
+    if (policy == POLICY_LIBSODIUM_1_0_18) {
+      ok &= !enc_small_order(Rw);
+      ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
+    }
+  } else {
+    ok = enc_y_canonical(Rw);
+  }
+  ok &= gu_frombytes(P, side ? Rw : Aw);
+  if (side) ok &= !(fu_iszero(P.X) & (int)(Rw[7] >> 31));
+  AT2V_PHASE(1);
+  uint32_t k[8];
+  {
+    uint32_t pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = Rw[i];
+      pre[8 + i] = Aw[i];
+    }
+    uint64_t h[8];
+    sha512_prefixed<16>(h, pre, len, msgword);
+    uint32_t hw[16];
+    sha512_digest_words(hw, h);
+    sc_reduce512(k, hw);
+  }
+  AT2V_PHASE(5);
+  HalfScalars hs;
+  lattice_reduce(hs, k);
+  AT2V_PHASE(7);
+  uint32_t t[8];
+  sc_mul_signed(t, hs, Sw);
+  uint32_t cd[8], td[8];
+  sc_recode4_hi8(cd, side ? hs.c1 : hs.c0);
+  sc_recode16(td, t);
+  ok &= hs.bits <= 255;
+  // the window count must cover both sides' scalars: every lane computes the same hs, so its own bits suffice
+  const int nw_lane = hs.bits <= 255 ? hs.bits / 4 + 1 : 0;
+  int nw = wave_max(nw_lane);
+  nw = nw < 30 ? 30 : nw;  // the top window (no B digit) must lie above the B windows 0, 4, ..., 28
+  AT2V_PHASE(2);
+  if (side && hs.c1_neg) {
+    fu_neg(P.X, P.X, FU_KC);
+    fu_carry(P.X);
+    fu_neg(P.T, P.T, FU_KC);
+    fu_carry(P.T);
+  }
+  {
+    gu_cached c1, cj;
+    gu_cached_identity(cj);
+    tp.store(0, cj);
+    gu_p3_to_cached(c1, P);
+    tp.store(1, c1);
+    gu_p3 Q = P;
+#pragma unroll 1
+    for (int j = 2; j <= 8; ++j) {
+      gu_p1p1 s;
+      gu_add(s, Q, c1);
+      gu_p1p1_to_p3(Q, s);
+      gu_p3_to_cached(cj, Q);
+      tp.store(j, cj);
+    }
+  }
+  AT2V_PHASE(3);
+  gu_p2 R2;
+  gu_p3 R3;
+  gu_p1p1 tt;
+  gu_cached ca;
+  gu_niels nb;
+  auto digit4 = [](const uint32_t d[8], int i) -> int { return (int)((sel8(d, i >> 3) >> (4 * (i & 7))) & 15) - 7; };
+  {
+    const int d = digit4(cd, nw - 1);
+    tp.prefetch(d < 0 ? -d : d);
+    gu_p3_identity(R3);
+    tp.load_prefetched(ca);
+    gu_cached_cneg(ca, d < 0);
+    gu_add(tt, R3, ca);
+    gu_p1p1_to_p2(R2, tt);
+  }
+  for (int i = nw - 2; i >= 0; --i) {
+    const int d = digit4(cd, i);
+    tp.prefetch(d < 0 ? -d : d);  // lands while the window's four doublings run
+    for (int r = 0; r < 3; ++r) {
+      gu_p2_dbl(tt, R2);
+      gu_p1p1_to_p2(R2, tt);
+    }
+    gu_p2_dbl(tt, R2);
+    gu_p1p1_to_p3(R3, tt);
+    const bool bwin = (i & 3) == 0 && i < 32;
+    int e = 0;
+    if (bwin)  // -t digit j = i/4 of this side's half: table [j]B (side 0) or [j 2^128]B (side 1)
+      e = (1 << 15) - (int)((sel8(td, (side ? 4 : 0) + (i >> 3)) >> (16 * ((i >> 2) & 1))) & 0xffff);
+    tp.load_prefetched(ca);
+    if (bwin) tb.prefetch(e < 0 ? -e : e);
+    gu_cached_cneg(ca, d < 0);
+    gu_add(tt, R3, ca);
+    if (bwin) {
+      gu_p1p1_to_p3(R3, tt);
+      tb.load_prefetched(nb);
+      gu_niels_cneg(nb, e < 0);
+      gu_madd(tt, R3, nb);
+    }
+    if (i > 0) gu_p1p1_to_p2(R2, tt);
+  }
+  gu_p1p1_to_p3(out, tt);
+  AT2V_PHASE(4);
+  return ok;
+}
+
+// V = mine + partner (the partner's point in cached form) == identity: in p1p1 (E, H, G, F), x = E/G and y = H/F,
+// so V = (0, 1) <=> E = 0 and H = F
+AT2V_HD AT2V_INLINE int verify_pair_combine(const gu_p3& mine, const gu_cached& partner) {
+  gu_p1p1 v;
+  gu_add(v, mine, partner);
+  fu d;
+  fu_sub(d, v.T, v.Y, FU_K2C);  // F + K - H: H = B + A is a sum of two carried elements, F may exceed FU_KC
+  return fu_iszero(v.X) & fu_iszero(d);
 }
 
 }  // namespace at2v

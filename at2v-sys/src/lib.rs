@@ -68,7 +68,12 @@ pub struct At2vOpts {
     pub device: c_int,
     pub num_gpus: c_int,
     pub policy: c_int,
+    /// launches of at most this many records run the low-latency kernel; 0 = 32768, AT2V_SMALL_BATCH_OFF = never
+    pub small_batch_max: u32,
 }
+
+pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
+pub const AT2V_SMALL_BATCH_OFF: u32 = 0xffffffff;
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
@@ -92,7 +97,11 @@ pub struct At2vQueueOpts {
     pub max_delay_us: u32,
     pub max_msg_bytes: u32,
     pub depth: u32,
+    pub flags: u32,
 }
+
+/// `At2vQueueOpts::flags`: also seal the filling batch whenever no batch is in flight (latency mode).
+pub const AT2V_QUEUE_EAGER: u32 = 1;
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]

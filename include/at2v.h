@@ -37,7 +37,11 @@ typedef struct {
   int device;         /* first HIP device ordinal (default 0) */
   int num_gpus;       /* devices device..device+num_gpus-1 share each host batch by index range; 0 or 1 = one GPU */
   at2v_policy policy; /* verdict semantics */
+  uint32_t small_batch_max; /* launches of at most this many records run the low-latency kernel (two lanes per
+                               record, one wave per SIMD); 0 = 32768; AT2V_SMALL_BATCH_OFF = never */
 } at2v_opts;
+#define AT2V_SMALL_BATCH_DEFAULT 32768u
+#define AT2V_SMALL_BATCH_OFF 0xffffffffu
 
 enum {
   AT2V_OK = 0,
@@ -147,8 +151,9 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
 /* ---- ingest/batching queue: the server's verify call site ----
  * Replaces the per-payload verify that sieve/murmur run on num_cpus::get() workers (rpc.rs:125,
  * rpc.rs:275-284 -> rpc.rs:156). Producers submit records; a batch is sealed at max_batch records, when
- * its oldest record is max_delay_us old, or on at2v_queue_flush(), and verified on the GPU
- * asynchronously (depth slots: one filling, up to depth-1 in flight). Verdicts come back in ticket
+ * its oldest record is max_delay_us old, or on at2v_queue_flush() — and, with AT2V_QUEUE_EAGER, whenever
+ * no batch is in flight (latency mode) — and verified on the GPU asynchronously (depth slots: one
+ * filling, up to depth-1 in flight). Verdicts come back in ticket
  * (= submission) order. Thread-safe: any number of producer threads; poll from any thread. */
 typedef struct at2v_queue at2v_queue;
 typedef struct {
@@ -158,7 +163,9 @@ typedef struct {
   uint32_t max_delay_us;  /* deadline of the oldest pending record; 0 = 1000 */
   uint32_t max_msg_bytes; /* message bytes budgeted per record (slot capacity max_batch x this); 0 = 256 */
   uint32_t depth;         /* batch slots, >= 2; 0 = 3 */
+  uint32_t flags;         /* AT2V_QUEUE_EAGER: also seal whenever no batch is in flight */
 } at2v_queue_opts;
+#define AT2V_QUEUE_EAGER 1u
 typedef struct {
   uint64_t submitted, completed, batches, failed_batches;
   double mean_batch;           /* records per completed batch */

@@ -1,7 +1,7 @@
 // queue_host.cpp — TEST ONLY: the product's batching queue (at2-node_amd/csrc/at2v_queue.h) driven on
 // the CPU with the oracle as its verify backend, to check flush policy, ticket order and verdict mapping
 // without a GPU. The shipped queue is instantiated with the HIP backend in at2v_host.hip.
-// usage: queue_host <scenario>   scenario in {order, size, deadline, flush, drain, startfail, failed}; exit 0 = pass
+// usage: queue_host <scenario>   scenario in {order, size, deadline, flush, eager, drain, startfail, failed}; exit 0 = pass
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -202,6 +202,40 @@ int scenario_deadline() {
   return 0;
 }
 
+int scenario_eager() {
+  // eager (latency) mode: with nothing in flight a lone record is launched at once, not at the deadline; records
+  // that arrive while a batch verifies form the next batch
+  Records r(40, 48);
+  OracleBackend be;
+  QueueOpts o;
+  o.max_batch = 4096;
+  o.max_delay_us = 30000000;  // 30 s: only the eager rule can seal within the test
+  o.max_msg_bytes = 48;
+  o.depth = 3;
+  o.eager = true;
+  BatchQueue<OracleBackend> q(be, o);
+  REQUIRE(q.start() == 0);
+  std::vector<uint8_t> got(r.n, 0xee);
+  std::vector<uint64_t> order;
+  const uint64_t t0 = now_us();
+  REQUIRE(q.submit(r.pk.data(), r.sig.data(), r.msg.data(), r.off.data(), 1, nullptr) == 0);
+  REQUIRE(drain(q, got, order, 1, 5000000) == 1);
+  const uint64_t dt1 = now_us() - t0;
+  // a burst of single-record submits: fewer batches than records, every verdict in ticket order
+  for (size_t i = 1; i < r.n; ++i) {
+    std::vector<uint32_t> o1 = {0, (uint32_t)r.L};
+    REQUIRE(q.submit(&r.pk[32 * i], &r.sig[64 * i], &r.msg[r.L * i], o1.data(), 1, nullptr) == 0);
+  }
+  REQUIRE(drain(q, got, order, r.n, 20000000) == (long)r.n);
+  const QueueStats s = q.stats();
+  printf("eager first_us=%llu batches=%llu mean_batch=%.2f\n", (unsigned long long)dt1, (unsigned long long)s.batches,
+         s.mean_batch);
+  REQUIRE(dt1 < 5000000);
+  REQUIRE(s.batches >= 2 && s.batches < r.n);
+  for (size_t i = 0; i < r.n; ++i) REQUIRE(got[i] == r.want[i] && order[i] == i);
+  return 0;
+}
+
 int scenario_flush() {
   Records r(5, 32);
   OracleBackend be;
@@ -299,6 +333,7 @@ int main(int argc, char** argv) {
   if (!strcmp(s, "size")) return scenario_size();
   if (!strcmp(s, "deadline")) return scenario_deadline();
   if (!strcmp(s, "flush")) return scenario_flush();
+  if (!strcmp(s, "eager")) return scenario_eager();
   if (!strcmp(s, "drain")) return scenario_drain();
   if (!strcmp(s, "startfail")) return scenario_startfail();
   if (!strcmp(s, "failed")) return scenario_failed();

@@ -117,7 +117,8 @@ int main(int argc, char** argv) {
   (void)ok;
   size_t bad_d = 0, bad_s = 0;
   int limit = argc > 2 ? atoi(argv[2]) : (int)n;
-  const int half = argc > 3 ? atoi(argv[3]) : 0;  // 1: the half-size equation (verify_half); 2: on the unsigned field
+  // 1: the half-size equation (verify_half); 2: on the unsigned field; 3: two lanes per signature (verify_pair_part)
+  const int half = argc > 3 ? atoi(argv[3]) : 0;
   for (size_t i = 0; i < n && (int)i < limit; ++i) {
     uint32_t R[8], A[8], S[8];
     words(R, &sig[64 * i]);
@@ -133,7 +134,23 @@ int main(int argc, char** argv) {
     static HostTabB16 tb;
     HostTabA ta, tr;
     int d, s;
-    if (half == 2) {
+    if (half == 3) {
+      static HostTabB16Hi tb1s;
+      static HostTabBFu<HostTabB16> fb0(tb);
+      static HostTabBFu<HostTabB16Hi> fb1(tb1s);
+      auto one = [](int v) { return v; };
+      auto pair = [&](int policy) {
+        HostTabAFu f0, f1;
+        gu_p3 P0, P1;
+        const int ok0 = verify_pair_part(0, R, A, S, len, mw, policy, f0, fb0, one, P0);
+        const int ok1 = verify_pair_part(1, R, A, S, len, mw, policy, f1, fb1, one, P1);
+        gu_cached c1;
+        gu_p3_to_cached(c1, P1);
+        return ok0 & ok1 & verify_pair_combine(P0, c1);
+      };
+      d = pair(POLICY_DALEK_V1);
+      s = pair(POLICY_LIBSODIUM_1_0_18);
+    } else if (half == 2) {
       static HostTabB16Hi tb1s;
       static HostTabBFu<HostTabB16> fb0(tb);
       static HostTabBFu<HostTabB16Hi> fb1(tb1s);

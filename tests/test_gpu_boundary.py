@@ -101,3 +101,19 @@ def test_config5_mininode_4_nodes(at2v_mod):
         json.dump(r, fp, indent=1)
     assert r["ledgers_identical"] and r["all_real_applied"] and r["bad_signatures"] > 0
     assert all(p["failed"] == 0 and p["rejected"] == r["bad_signatures"] for p in r["per_node"])
+
+
+@pytest.mark.timeout(600)
+def test_config5_mininode_eager_latency(at2v_mod):
+    """BASELINE config 5 in the queue's latency mode (seal whenever no batch is in flight) with the low-latency
+    kernel: same correctness bar as above; the measured latency goes to gpurun_out/config5_eager.json"""
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mininode.py"), "--nodes", "4", "--rate", "20000",
+                          "--seconds", "2", "--batch", "1024", "--delay-us", "1000", "--eager", "1"],
+                         capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    with open(os.path.join(ROOT, "gpurun_out", "config5_eager.json"), "w") as fp:
+        json.dump(r, fp, indent=1)
+    assert r["ledgers_identical"] and r["all_real_applied"] and r["bad_signatures"] > 0
+    assert all(p["failed"] == 0 and p["rejected"] == r["bad_signatures"] for p in r["per_node"])

@@ -22,16 +22,21 @@ def at2v_mod():
     return at2v
 
 
-@pytest.fixture(scope="module")
-def verifier(at2v_mod):
-    v = at2v_mod.BatchVerifier(policy="dalek")
+# Both verify kernels: "lowlat" = the library default (launches of <= 32768 records run the two-lanes-per-record
+# kernel, larger ones the throughput kernel); "throughput" = the throughput kernel at every size.
+KERNELS = {"lowlat": 0, "throughput": 0xFFFFFFFF}
+
+
+@pytest.fixture(scope="module", params=list(KERNELS))
+def verifier(at2v_mod, request):
+    v = at2v_mod.BatchVerifier(policy="dalek", small_batch_max=KERNELS[request.param])
     yield v
     v.close()
 
 
-@pytest.fixture(scope="module")
-def verifier_sodium(at2v_mod):
-    v = at2v_mod.BatchVerifier(policy="libsodium")
+@pytest.fixture(scope="module", params=list(KERNELS))
+def verifier_sodium(at2v_mod, request):
+    v = at2v_mod.BatchVerifier(policy="libsodium", small_batch_max=KERNELS[request.param])
     yield v
     v.close()
 
@@ -214,3 +219,16 @@ def test_many_chunks_per_wave_adversarial(verifier, oracle):
     got = verifier.verify_batch(pk, sig, msg, off)
     assert np.array_equal(got, want), _mismatch(got, want, cls)
     assert 0.85 * n < want.sum() < n
+
+
+def test_lowlat_kernel_grid_stride(at2v_mod, oracle):
+    """the two-lanes-per-record kernel forced on a batch larger than one pass of its grid (grid-strided 32-record
+    chunks), against the oracle"""
+    pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 7, 0, 100_000, 64)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    v = at2v_mod.BatchVerifier(policy="dalek", small_batch_max=1 << 20)
+    try:
+        got = v.verify_batch(pk, sig, msg, off)
+    finally:
+        v.close()
+    assert np.array_equal(got, want), _mismatch(got, want, cls)

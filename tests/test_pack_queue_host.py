@@ -99,7 +99,7 @@ def queue_host():
 
 
 @pytest.mark.parametrize("build", list(SANITIZE))
-@pytest.mark.parametrize("scenario", ["order", "size", "deadline", "flush", "drain", "startfail", "failed"])
+@pytest.mark.parametrize("scenario", ["order", "size", "deadline", "flush", "eager", "drain", "startfail", "failed"])
 def test_queue_core_on_host(queue_host, scenario, build):
     """order: 4 producer threads, random run lengths, verdicts map back through tickets (oracle backend);
     size: a full batch seals at max_batch; deadline: a partial batch seals at max_delay_us;

@@ -125,11 +125,11 @@ def test_constants_match_header():
     txt = open(HEADER).read()
     src = open(os.path.join(CRATE, "src", "lib.rs")).read()
     consts = dict(re.findall(r"\b(AT2V_[A-Z0-9_]+)\s*=\s*(-?\d+)", txt))
-    consts.update(re.findall(r"#define (AT2V_[A-Z0-9_]+) (\d+)", txt))
+    consts.update(re.findall(r"#define (AT2V_[A-Z0-9_]+) ((?:0x)?[0-9a-fA-F]+)u?\b", txt))
     rust = dict(re.findall(r"pub const (AT2V_[A-Z0-9_]+): \w+ = (-?(?:0x)?[0-9a-f]+);", src))
     for k, v in consts.items():
         assert k in rust, k
-        assert int(rust[k], 0) == int(v), (k, rust[k], v)
+        assert int(rust[k], 0) == int(v, 0), (k, rust[k], v)
 
 
 def test_build_script_links_libat2v():

@@ -45,6 +45,8 @@ __device__ __forceinline__ void at2v_phase_mark(int k) {
 
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 20);
+  // launches of <= pair_max records run the two-lanes-per-record kernel (0: always the throughput kernel)
+  const uint32_t pair_max = argc > 2 ? (uint32_t)atoi(argv[2]) : 0u;
   const uint32_t L = 100;
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, 0));
@@ -80,7 +82,7 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
     CHECK(hipEventRecord(e0, 0));
-    CHECK(at2v::launch_verify(pk, sig, msg, n * L, off, n, 0, ver, scratch, btab, grid, 0));
+    CHECK(at2v::launch_verify(pk, sig, msg, n * L, off, n, 0, ver, scratch, btab, grid, pair_max, 0));
     CHECK(hipEventRecord(e1, 0));
     CHECK(hipEventSynchronize(e1));
     CHECK(hipEventElapsedTime(&ms, e0, e1));
