@@ -33,8 +33,9 @@ CFG_SEED = 0x4154325F
 FIELD_MUL_PER_VERIFY = 1195
 FIELD_SQ_PER_VERIFY = 1022
 MAC_PER_VERIFY = 100 * FIELD_MUL_PER_VERIFY + 55 * FIELD_SQ_PER_VERIFY  # 175,710
-# Peak: v_mad_i64_i32 issues at half the VALU rate on gfx950 (profiles/r01_ubench_valu.txt): one wave64
-# instruction per 4 cycles per SIMD = 16 lane-MACs/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz.
+# Peak: v_mad_u64_u32 (the MAC of the unsigned-limb field; v_mad_i64_i32 alike) issues at half the
+# VALU rate on gfx950 (profiles/r01_ubench_valu.txt): one wave64 instruction per 4 cycles per SIMD
+# = 16 lane-MACs/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz.
 MAC_PEAK = 256 * 4 * 16 * 2.4e9  # 3.93e13 MAC/s
 HBM_PEAK_GBS = 8000.0
 
@@ -254,7 +255,7 @@ def main():
                 "bound": "valu",
                 "achieved": achieved,
                 "peak": MAC_PEAK / 1e12,
-                "unit": "Tops/s (32x32->64 integer MAC, v_mad_i64_i32)",
+                "unit": "Tops/s (32x32->64 integer MAC, v_mad_u64_u32)",
                 "frac": achieved * 1e12 / MAC_PEAK,
                 "traffic": None,
                 "alg_macs_per_verify": MAC_PER_VERIFY,
@@ -440,7 +441,7 @@ def pmc_traffic(args, n, L):
 
 def pmc_valu(args, n, L):
     """Measured VALU work and issue rate of the verify kernel (SURVEY 8(d) '% VALU peak'), one PMC pass:
-    SQ_INSTS_VALU (wave instructions), its INT64 part (v_mad_i64_i32, 64-bit shifts/adds: half rate on
+    SQ_INSTS_VALU (wave instructions), its INT64 part (v_mad_u64_u32, 64-bit shifts/adds: half rate on
     gfx950) and GRBM_GUI_ACTIVE (summed over the 8 XCDs -> effective clock, MI355X guide 'DVFS give-back').
     Issue fraction: nominal SIMD cycles of the mix (half-rate wave64 op 4 cycles, full-rate 2; every non-INT64
     op is priced at 2, so this is a lower bound) over the cycles the 1024 SIMDs had at the effective clock."""

@@ -29,7 +29,8 @@ def host_exe_asan():
     return exe
 
 
-@pytest.mark.parametrize("half", [0, 1, 2], ids=["full_length", "half_size", "half_size_unsigned_field"])
+@pytest.mark.parametrize("half", [0, 1, 2, 3], ids=["full_length", "half_size", "half_size_unsigned_field",
+                                                   "two_lanes_per_record"])
 def test_sanitized_host_build_of_device_core(host_exe_asan, half):
     """the same code under AddressSanitizer + UBSan (signed overflow, shifts, bounds) over the edge and
     adversarial fixtures"""
@@ -39,11 +40,13 @@ def test_sanitized_host_build_of_device_core(host_exe_asan, half):
         assert out.returncode == 0, out.stderr[-3000:]
 
 
-@pytest.mark.parametrize("half", [0, 1, 2], ids=["full_length", "half_size", "half_size_unsigned_field"])
+@pytest.mark.parametrize("half", [0, 1, 2, 3], ids=["full_length", "half_size", "half_size_unsigned_field",
+                                                   "two_lanes_per_record"])
 @pytest.mark.parametrize("name", golden_io.SETS)
 def test_host_build_of_device_core_matches_golden(host_exe, name, half):
-    """every verify form the kernel can be built with: the full-length ladder (verify_core), the half-size lattice
-    form on the signed field (verify_half) and on the unsigned chained-carry field (verify_half_fu, the default),
+    """every verify form the kernels can be built with: the full-length ladder (verify_core), the half-size lattice
+    form on the signed field (verify_half) and on the unsigned chained-carry field (verify_half_fu, the throughput
+    kernel), and its two-lanes-per-record split (verify_pair_part + verify_pair_combine, the low-latency kernel),
     against OpenSSL/libsodium-derived verdicts"""
     out = subprocess.run([host_exe, os.path.join(golden_io.GOLDEN_DIR, name + ".bin"), "1000000", str(half)],
                          capture_output=True, text=True, timeout=600)
