@@ -33,11 +33,18 @@ inline uint64_t at2v_umad_checked(uint64_t a, uint64_t b, uint64_t c) {
   if ((uint64_t)(r >> 64)) { fprintf(stderr, "fu column overflow\n"); abort(); }
   return (uint64_t)r;
 }
+inline uint32_t at2v_unarrow_checked(uint64_t c) {
+  if (c >> 32) { fprintf(stderr, "fu narrow wrap overflow %llu\n", (unsigned long long)c); abort(); }
+  return (uint32_t)c;
+}
 #define AT2V_UMAD(a, b, c) at2v_umad_checked((uint32_t)(a), (uint32_t)(b), (uint64_t)(c))
 #define AT2V_USC(s, x) at2v_usc_checked((s), (x))
+#define AT2V_UNARROW(c) at2v_unarrow_checked(c)
 #else
 #define AT2V_UMAD(a, b, c) ((uint64_t)(uint32_t)(a) * (uint64_t)(uint32_t)(b) + (uint64_t)(c))
 #define AT2V_USC(s, x) ((s) * (x))
+// top carry known (tools/gen_fu.py check_group_law) to be below 2^32: the one-MAD wrap
+#define AT2V_UNARROW(c) ((uint32_t)(c))
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)

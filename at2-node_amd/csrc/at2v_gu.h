@@ -6,6 +6,8 @@
 // by tools/gen_fu.py (check_group_law mirrors this file). Conventions:
 //   p1p1 (X, Y, Z, T) represents x = X/Z, y = Y/T; X may be "wide" (fu_mul f-side only), Y, Z, T are g-side operands.
 //   p1p1 -> p2/p3: X3 = X*T, Y3 = Y*Z, Z3 = Z*T (, T3 = X*Y) — the first operand is fu_mul's f.
+// Products whose inputs keep the top carry below 2^32 (proven per site by check_group_law) use the one-MAD wrap
+// variants (fu_mul_n / _wn / _nn, fu_sqc_x2, fu_sq_sq2_n).
 #pragma once
 #include "at2v_fu.h"
 
@@ -25,12 +27,12 @@ AT2V_HD AT2V_INLINE void gu_p3_identity(gu_p3& p) {
 }
 
 AT2V_HD AT2V_INLINE void gu_p1p1_to_p2(gu_p2& r, const gu_p1p1& p) {
-  fu_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fu_mul_wn(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fu_mul(r.Z, p.Z, p.T);
 }
 
 AT2V_HD AT2V_INLINE void gu_p1p1_to_p3(gu_p3& r, const gu_p1p1& p) {
-  fu_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fu_mul_wn(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fu_mul_x2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
 }
 
@@ -40,8 +42,8 @@ AT2V_HD AT2V_INLINE void gu_p1p1_to_p3(gu_p3& r, const gu_p1p1& p) {
 AT2V_HD AT2V_INLINE void gu_p2_dbl(gu_p1p1& r, const gu_p2& p) {
   fu XX, YY, ZZ2, s, t0;
   fu_add(s, p.X, p.Y);
-  fu_sq_x2(XX, p.X, YY, p.Y);
-  fu_sq_sq2(t0, s, ZZ2, p.Z);
+  fu_sqc_x2(XX, p.X, YY, p.Y);
+  fu_sq_sq2_n(t0, s, ZZ2, p.Z);
   fu_add(r.Y, XX, YY);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -64,8 +66,8 @@ AT2V_HD AT2V_INLINE void gu_add(gu_p1p1& r, const gu_p3& p, const gu_cached& q) 
   fu a, b, c, d, ym, yp;
   fu_sub(ym, p.Y, p.X, FU_KC);
   fu_add(yp, p.Y, p.X);
-  fu_mul_x2(a, ym, q.YmX, b, yp, q.YpX);
-  fu_mul_x2(c, p.T, q.T2d, d, p.Z, q.Z2);
+  fu_mul_wn(a, ym, q.YmX, b, yp, q.YpX);
+  fu_mul_nn(c, p.T, q.T2d, d, p.Z, q.Z2);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     r.X.v[i] = b.v[i] + FU_KC.v[i] - a.v[i];  // E
@@ -80,8 +82,8 @@ AT2V_HD AT2V_INLINE void gu_madd(gu_p1p1& r, const gu_p3& p, const gu_niels& q) 
   fu a, b, c, ym, yp;
   fu_sub(ym, p.Y, p.X, FU_KC);
   fu_add(yp, p.Y, p.X);
-  fu_mul_x2(a, ym, q.ymx, b, yp, q.ypx);
-  fu_mul(c, p.T, q.xy2d);
+  fu_mul_nn(a, ym, q.ymx, b, yp, q.ypx);
+  fu_mul_n(c, p.T, q.xy2d);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     const uint32_t d = p.Z.v[i] + p.Z.v[i];
@@ -97,7 +99,7 @@ AT2V_HD AT2V_INLINE void gu_p3_to_cached(gu_cached& r, const gu_p3& p) {
   fu_add(r.YpX, p.Y, p.X);
   fu_sub(r.YmX, p.Y, p.X, FU_KC);
   fu_add(r.Z2, p.Z, p.Z);
-  fu_mul(r.T2d, p.T, FU_D2);
+  fu_mul_n(r.T2d, p.T, FU_D2);
 }
 
 AT2V_HD AT2V_INLINE void gu_cached_identity(gu_cached& r) {

@@ -164,19 +164,28 @@ def kconst(dom):
     return best[1]
 
 
+MCOLS = build_cols(mul_terms())
+
+
 class Model:
-    """the group-law formulas of at2v_gu.h on per-limb maxima: checks product inputs against the classes"""
+    """the group-law formulas of at2v_gu.h on per-limb maxima: checks product inputs against the classes, and for
+    the products emitted with the one-MAD wrap (`narrow`, the fu_*_n / *_wn / *_nn variants) that the top carry of
+    that site's inputs stays below 2^32"""
 
     def __init__(self, carried):
         self.C = carried
 
-    def mul(self, f, g, where):
+    def mul(self, f, g, where, narrow=False):
         assert all(f[i] <= MUL_F[i] for i in range(10)), (where, "f", f)
         assert all(g[i] <= MUL_G[i] for i in range(10)), (where, "g", g)
+        if narrow:
+            assert prove(MCOLS, f, g, where)[1] < 2**32, where
         return self.C
 
-    def sq(self, f, where):
+    def sq(self, f, where, narrow=False, double=False):
         assert all(f[i] <= SQ_IN[i] for i in range(10)), (where, f)
+        if narrow:
+            assert prove(build_cols(sq_terms(double, SQ_IN)), f, f, where)[1] < 2**32, where
         return self.C
 
 
@@ -199,32 +208,36 @@ def check_group_law(C, K):
     #     N1 = XX + YY + K - t0 (= -2XY), D1 = XX + K - YY (= X^2 - Y^2), N2 = XX + YY, D2 = ZZ2 + D1, even-carried
     X = Y = Z = C
     s = add(X, Y)
-    XX = m.sq(X, "dbl XX"); YY = m.sq(Y, "dbl YY"); t0 = m.sq(s, "dbl (X+Y)^2"); ZZ2 = m.sq(Z, "dbl 2Z^2")
+    XX = m.sq(X, "dbl XX", True); YY = m.sq(Y, "dbl YY", True)
+    t0 = m.sq(s, "dbl (X+Y)^2", True); ZZ2 = m.sq(Z, "dbl 2Z^2", True, True)
     N2 = add(XX, YY)
     assert dom(KC, t0) and dom(KC, YY)
     N1 = add(N2, KC)
     D1 = add(XX, KC)
     D2 = pcarry_even(add(ZZ2, D1))
-    # p1p1 (X, Y, Z, T) = (N1, N2, D1, D2); products X = N1 D2, Y = N2 D1, Z = D1 D2, T = N1 N2
-    m.mul(N1, D2, "dbl X"); m.mul(N2, D1, "dbl Y"); m.mul(D2, D1, "dbl Z"); m.mul(N1, N2, "dbl T")
+    dbl = (N1, N2, D1, D2)
     # --- addition p3 + cached -> p1p1 (gu_add); cached entries as stored by gu_p3_to_cached
     ypx, ymx, z2, t2d = add(C, C), add(C, KC), add(C, C), C
     assert dom(KC, C)
     ym = add(C, KC); yp = add(C, C)
     for (pp, mm) in ((ypx, ymx), (ymx, ypx)):    # a negative digit swaps YpX / YmX and negates T2d
-        m.mul(ym, mm, "add A"); m.mul(yp, pp, "add B")
-    m.mul(C, add(KC, [0] * 10), "add C (negated T2d: K - T2d)") if False else None
+        m.mul(ym, mm, "add A"); m.mul(yp, pp, "add B", True)
     tneg = KC                                        # K_C - T2d <= K_C
-    m.mul(C, t2d, "add C"); m.mul(C, tneg, "add C-"); m.mul(C, z2, "add D")
+    m.mul(C, t2d, "add C", True); m.mul(C, tneg, "add C-", True); m.mul(C, z2, "add D", True)
     Ea = add(C, KC); Ha = add(C, C); Ga = add(C, C); Fa = add(C, KC)
-    m.mul(Ea, Fa, "add X"); m.mul(Ha, Ga, "add Y"); m.mul(Ga, Fa, "add Z"); m.mul(Ea, Ha, "add T")
+    addr = (Ea, Ha, Ga, Fa)
     # --- mixed addition with an affine Niels entry (gu_madd): entries carried; negation as for cached
-    m.mul(ym, C, "madd A"); m.mul(yp, C, "madd B"); m.mul(C, C, "madd C"); m.mul(C, KC, "madd C-")
+    m.mul(ym, C, "madd A", True); m.mul(yp, C, "madd B", True); m.mul(C, C, "madd C", True)
+    m.mul(C, KC, "madd C-", True)
     d2 = add(C, C)
-    Gm = add(d2, C); Fm = add(d2, KC)
-    m.mul(Fm, Ea, "madd X"); m.mul(Gm, Ha, "madd Y"); m.mul(Fm, Gm, "madd Z"); m.mul(Ea, Ha, "madd T")
+    Gm = add(d2, C); Fm = pcarry_even(add(d2, KC))
+    madd = (Ea, Ha, Gm, Fm)
+    # p1p1 (X, Y, Z, T) -> p2 / p3 (gu_p1p1_to_p2 / _p3): X3 = X T (wide), Y3 = Y Z (narrow), Z3 = Z T (wide),
+    # T3 = X Y (wide)
+    for (x, y, z, t), nm in ((dbl, "dbl"), (addr, "add"), (madd, "madd")):
+        m.mul(x, t, nm + " X"); m.mul(y, z, nm + " Y", True); m.mul(z, t, nm + " Z"); m.mul(x, y, nm + " T")
     # --- cached form of a p3 point: YpX = Y + X, YmX = Y + K_C - X, Z2 = 2Z, T2d = T * 2d
-    m.mul(C, C, "T2d")
+    m.mul(C, C, "T2d", True)
     # --- decode: u = y^2 + (p - 1), v = d y^2 + 1; checks on v x^2 -+ u
     u = add(C, K["PM1"])
     v = add(C, [1] + [0] * 9)
@@ -325,7 +338,7 @@ def emit_fn(name, colsets, is_mul, cheap_wrap):
     for q, cw in zip(ps, cheap_wrap):
         out.append("  {")
         if cw:  # c9 < 2^32 (proven): one 32x32+64 MAD
-            out.append(f"    const uint64_t t = AT2V_UMAD((uint32_t)c{q}, 19u, h{q}.v[0]);")
+            out.append(f"    const uint64_t t = AT2V_UMAD(AT2V_UNARROW(c{q}), 19u, h{q}.v[0]);")
         else:
             out.append(f"    const uint64_t t = (uint64_t)h{q}.v[0] + 19u * c{q};")
         out.append(f"    h{q}.v[0] = (uint32_t)t & 0x3ffffffu;")
@@ -390,6 +403,11 @@ def main():
     hdr.append(emit_fn("fu_mulc", [mcols], True, [True]))
     hdr.append(emit_fn("fu_sqc", [sccols], False, [True]))
     hdr.append(emit_fn("fu_mulc_x2", [mcols, mcols], True, [True, True]))
+    hdr.append("// one-MAD wrap at the sites check_group_law proves narrow (n), full wrap where it does not (w)")
+    hdr.append(emit_fn("fu_mul_n", [mcols], True, [True]))
+    hdr.append(emit_fn("fu_mul_wn", [mcols, mcols], True, [cw_m, True]))
+    hdr.append(emit_fn("fu_mul_nn", [mcols, mcols], True, [True, True]))
+    hdr.append(emit_fn("fu_sq_sq2_n", [scols, s2cols], False, [True, True]))
     hdr.append(emit_fn("fu_sqc_x2", [sccols, sccols], False, [True, True]))
     hdr.append("// subtraction constants (multiples of p): FU_KC dominates a carried element, FU_K2C a sum of two carried")
     hdr.append(f"AT2V_FU_CONST fu FU_KC = {lit(K['C'])};")
