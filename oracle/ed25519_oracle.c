@@ -14,6 +14,12 @@
  * Policy LIBSODIUM_1_0_18 adds libsodium 1.0.18's pre-rejects (Appendix A.4).
  *
  * Field: GF(2^255-19) as 5 x 51-bit limbs (u64), products in unsigned __int128.
+ *
+ * Parity status: UNPINNED against the reference itself. at2-node holds no vectors for this path and its verify
+ * lives in the unvendored, unbuildable drop -> ed25519-dalek dependency. What pins this restatement
+ * instead: RFC 8032 §7.1 TEST 1-3, OpenSSL 3.0.2 EVP_DigestVerify (dalek-1.x semantics on every probed edge class)
+ * and libsodium 1.0.18 (strict policy), 0 mismatches over 13,220 fixture records (oracle/crosscheck.c,
+ * tests/golden/crosscheck.log).
  */
 #include "ed25519_oracle.h"
 

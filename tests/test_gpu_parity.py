@@ -232,3 +232,17 @@ def test_lowlat_kernel_grid_stride(at2v_mod, oracle):
     finally:
         v.close()
     assert np.array_equal(got, want), _mismatch(got, want, cls)
+
+
+
+def test_ragged_long_messages(verifier, oracle):
+    """Messages of very different lengths inside one wave (0 B up to 16 KiB, so lanes need 1 to 130 SHA-512 blocks),
+    at packed unaligned offsets, signed by the oracle signer; about a third mutated (message byte, S, R or A). Record by
+    record against the oracle; every unmutated record verifies and no mutated one does."""
+    import ragged_records
+    pk, sig, msg, off, mutated = ragged_records.make(oracle, 2500, seed=20261017)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    got = verifier.verify_batch(pk, sig, msg, off)
+    assert np.array_equal(got, want), _mismatch(got, want)
+    assert want[~mutated].all()
+    assert not want[mutated].any()

@@ -72,3 +72,14 @@ def test_verify_one_rejects_bad_arguments(at2v_mod):
     assert lib.at2v_verify_one_policy(b"\0" * 32, b"\0" * 64, None, 0, 7) == -1
     assert lib.at2v_verify_one(b"\0" * 32, b"\0" * 64, None, 5) == -1  # msg NULL with len > 0
     assert lib.at2v_verify_one(b"\0" * 32, b"\0" * 64, None, 0) == 0   # empty message is fine
+
+
+def test_verify_one_ragged_long_messages(at2v_mod, oracle):
+    """0 B .. 16 KiB messages (1 to 130 SHA-512 blocks), about a third mutated: the CPU drop-in against the oracle"""
+    import ragged_records
+    pk, sig, msg, off, mutated = ragged_records.make(oracle, 600, seed=7, n_long=60)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    got = np.array([at2v_mod.verify_one(pk[i].tobytes(), sig[i].tobytes(), msg[off[i]:off[i + 1]].tobytes())
+                    for i in range(len(pk))])
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert want[~mutated].all() and not want[mutated].any()
