@@ -511,10 +511,67 @@ def cpu_baseline(args, d_pk, d_sig, d_msg, n, L):
     t0 = time.perf_counter()
     ok = o.verify_batch(pk, sig, msg, off, 0, threads)
     dt = time.perf_counter() - t0
-    return {"value": m / dt, "unit": "verifies/s", "cores": threads, "kind": "port", **detail,
-            "sample": f"{m} records of the benchmark batch ({L}-byte M), oracle/ed25519_oracle.c, {threads} threads "
-                      f"(all usable cores), {dt:.2f} s wall; all valid={bool(ok.all())}; stand-in for the reference's "
-                      f"rayon ed25519-dalek path (not buildable offline)"}
+    out = {"value": m / dt, "unit": "verifies/s", "cores": threads, "kind": "port", **detail,
+           "sample": f"{m} records of the benchmark batch ({L}-byte M), oracle/ed25519_oracle.c, {threads} threads "
+                     f"(all usable cores), {dt:.2f} s wall; all valid={bool(ok.all())}; stand-in for the reference's "
+                     f"rayon ed25519-dalek path (not buildable offline)"}
+    ossl = openssl_baseline(d_pk, d_sig, d_msg, n, L, threads, rate0)
+    if ossl is not None:
+        out["openssl"] = ossl
+    return out
+
+
+def openssl_baseline(d_pk, d_sig, d_msg, n, L, threads, rate_hint):
+    """SURVEY 8(d)'s preferred CPU baseline: OpenSSL 3 libcrypto Ed25519 verify (EVP_DigestVerify) over the same
+    records, one pthread per usable core (oracle/openssl_verify.c, built by `make -C oracle openssl`); None when the
+    library is not there. Bounded sample, ~3 s of wall time."""
+    import ctypes
+
+    import numpy as np
+
+    path = os.path.join(ROOT, "oracle", "libossl_verify.so")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError:
+        return None
+    P = ctypes.c_void_p
+    lib.ossl_verify_batch.argtypes = [P, P, P, P, ctypes.c_size_t, ctypes.c_int, P]
+    lib.ossl_verify_batch.restype = ctypes.c_int
+
+    def run(m):
+        pk = np.ascontiguousarray(d_pk[: m * 32].cpu().numpy())
+        sig = np.ascontiguousarray(d_sig[: m * 64].cpu().numpy())
+        msg = np.ascontiguousarray(d_msg[: m * L].cpu().numpy())
+        off = (np.arange(m + 1) * L).astype(np.uint32)
+        res = np.zeros(m, dtype=np.uint8)
+        t0 = time.perf_counter()
+        rc = lib.ossl_verify_batch(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, off.ctypes.data, m, threads,
+                                   res.ctypes.data)
+        return time.perf_counter() - t0, rc, res
+
+    m0 = min(n, 64 * threads)
+    dt0, rc, _ = run(m0)  # warm-up and rate estimate
+    if rc != 0:
+        return None
+    m = int(min(n, max(m0, 3.0 * m0 / max(dt0, 1e-6))))
+    dt, rc, res = run(m)
+    if rc != 0:
+        return None
+    return {"value": m / dt, "unit": "verifies/s", "cores": threads, "kind": "third-party",
+            "sample": f"{m} records of the benchmark batch ({L}-byte M), OpenSSL {ossl_version(lib)} EVP_DigestVerify "
+                      f"(Ed25519), {threads} threads, {dt:.2f} s wall; all valid={bool(res.all())}; SURVEY 8(d)'s "
+                      f"preferred stand-in for the reference's rayon ed25519-dalek path"}
+
+
+def ossl_version(lib):
+    import ctypes
+    try:
+        f = lib.OpenSSL_version
+        f.restype = ctypes.c_char_p
+        f.argtypes = [ctypes.c_int]
+        return f(0).decode().split()[1]
+    except (AttributeError, OSError, IndexError):
+        return "3"
 
 
 if __name__ == "__main__":
