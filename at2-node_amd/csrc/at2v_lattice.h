@@ -147,6 +147,10 @@ AT2V_HD AT2V_INLINE void euclid_reduce(U256& a, U256& ma, const U256& b, const U
   }
 }
 
+#ifndef AT2V_LEHMER_IEEE_DIV
+#define AT2V_LEHMER_IEEE_DIV 0  // 1: IEEE float division in the Lehmer quotient estimate (A/B)
+#endif
+
 #ifndef AT2V_LATTICE_LEHMER
 #define AT2V_LATTICE_LEHMER 2  // 0: plain Euclid, 1: Lehmer on 62-bit leading parts, 2: on 30-bit parts
 #endif
@@ -233,7 +237,13 @@ AT2V_HD AT2V_INLINE void lehmer_round32(int& steps, int64_t& A64, int64_t& B64, 
     if (yc <= 0 || yd <= 0) break;
     if ((yc < yd ? yc : yd) <= chat) break;  // true v might be < thr
     const int32_t xa = x + A, xb = x + B;
+    // xa < 2^31, 1 <= yc, and only q < 32767 is used: a one-ulp reciprocal keeps |qf - xa/yc| < 2^-7, so the floor
+    // is exact or one off, which the correction below fixes (the IEEE division would cost ~12 instructions)
+#if defined(__HIP_DEVICE_COMPILE__) && !AT2V_LEHMER_IEEE_DIV
+    const float qf = (float)xa * __builtin_amdgcn_rcpf((float)yc);
+#else
     const float qf = (float)xa / (float)yc;
+#endif
     if (qf >= 32767.0f) break;                // keep q, cofactors and products inside 32 bits
     int32_t q = (int32_t)qf;
     int32_t r = xa - q * yc;  // fix the estimate to the exact floor (off by at most one)

@@ -44,6 +44,24 @@ AT2V_HD AT2V_INLINE uint64_t sha_ror(uint64_t x, int n) {
   return (x >> n) | (x << (64 - n));
 #endif
 }
+// x ^ y ^ z and maj(x, y, z) on 64-bit words; on gfx950 one v_bitop3_b32 per half (truth tables 0x96 and 0xe8,
+// both symmetric in their operands) instead of two XORs, or an XOR and a bit-select. AT2V_SHA_BITOP3=0: plain C.
+#ifndef AT2V_SHA_BITOP3
+#define AT2V_SHA_BITOP3 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && AT2V_SHA_BITOP3
+template <int LUT>
+__device__ AT2V_INLINE uint64_t sha_bitop3(uint64_t x, uint64_t y, uint64_t z) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, LUT);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), LUT);
+  return ((uint64_t)hi << 32) | lo;
+}
+AT2V_HD AT2V_INLINE uint64_t sha_xor3(uint64_t x, uint64_t y, uint64_t z) { return sha_bitop3<0x96>(x, y, z); }
+AT2V_HD AT2V_INLINE uint64_t sha_maj(uint64_t x, uint64_t y, uint64_t z) { return sha_bitop3<0xe8>(x, y, z); }
+#else
+AT2V_HD AT2V_INLINE uint64_t sha_xor3(uint64_t x, uint64_t y, uint64_t z) { return x ^ y ^ z; }
+AT2V_HD AT2V_INLINE uint64_t sha_maj(uint64_t x, uint64_t y, uint64_t z) { return (x & y) ^ (z & (x ^ y)); }
+#endif
 AT2V_HD AT2V_INLINE uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -57,11 +75,11 @@ AT2V_HD AT2V_INLINE void sha512_init(uint64_t h[8]) {
 // one round with the working variables passed in rotated order (no register moves between rounds)
 AT2V_HD AT2V_INLINE void sha512_round(uint64_t a, uint64_t b, uint64_t c, uint64_t& d, uint64_t e, uint64_t f,
                                       uint64_t g, uint64_t& h, uint64_t kw) {
-  const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
+  const uint64_t S1 = sha_xor3(sha_ror(e, 14), sha_ror(e, 18), sha_ror(e, 41));
   const uint64_t ch = (e & f) ^ (~e & g);
   const uint64_t t1 = h + S1 + ch + kw;
-  const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
-  const uint64_t mj = (a & b) ^ (c & (a ^ b));
+  const uint64_t S0 = sha_xor3(sha_ror(a, 28), sha_ror(a, 34), sha_ror(a, 39));
+  const uint64_t mj = sha_maj(a, b, c);
   d += t1;
   h = t1 + S0 + mj;
 }
@@ -73,8 +91,8 @@ AT2V_HD AT2V_INLINE void sha512_rounds16(uint64_t s[8], uint64_t w[16], int r0) 
   for (int i = 0; i < 16; ++i) {
     if (SCHED) {
       const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-      const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = sha_xor3(sha_ror(w15, 1), sha_ror(w15, 8), w15 >> 7);
+      const uint64_t s1 = sha_xor3(sha_ror(w2, 19), sha_ror(w2, 61), w2 >> 6);
       w[i] += s0 + w[(i + 9) & 15] + s1;
     }
     const uint64_t kw = SHA512_K[r0 + i] + w[i];
