@@ -246,3 +246,47 @@ def test_ragged_long_messages(verifier, oracle):
     assert np.array_equal(got, want), _mismatch(got, want)
     assert want[~mutated].all()
     assert not want[mutated].any()
+
+
+def test_config3_total_size_on_one_gpu(at2v_mod):
+    """BASELINE config 3's whole batch (16M signatures, here + 17 for a ragged tail) in ONE launch on one GPU: 262,145
+    chunks through the chunk queue, 1.68 GB of messages (offsets near the top of the u32 range the ABI allows).
+    Every generated record verifies; after mutating 3,000 random records in S, M or A exactly those are rejected,
+    and the pad bits of the last verdict word stay 0."""
+    import torch
+    n, L = (1 << 24) + 17, 100
+    v = at2v_mod.BatchVerifier(policy="dalek", small_batch_max=0xFFFFFFFF)
+    try:
+        s = torch.cuda.current_stream().cuda_stream
+        d_pk = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+        d_msg = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+        d_off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+        words = (n + 31) // 32
+        d_ver = torch.zeros(words, dtype=torch.int32, device="cuda")
+        v.gen_records_device(CFG_SEED + 3, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                             d_off.data_ptr(), s)
+        v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                              d_ver.data_ptr(), s)
+        torch.cuda.synchronize()
+        ok = at2v_mod.unpack_verdicts(d_ver.cpu().numpy().view(np.uint32), n)
+        assert ok.all(), f"{(~ok).sum()} generated records rejected"
+        rng = np.random.default_rng(33)
+        idx = np.unique(rng.integers(0, n, 3000))
+        which = rng.integers(0, 3, idx.size)
+        bits = torch.from_numpy((1 << rng.integers(0, 8, idx.size)).astype(np.uint8)).cuda()
+        for w, (arr, width) in enumerate(((d_sig, 64), (d_msg, L), (d_pk, 32))):
+            sel = np.nonzero(which == w)[0]
+            rows = torch.from_numpy(idx[sel]).cuda()
+            cols = torch.from_numpy(rng.integers(0, width, sel.size)).cuda()
+            view = arr.view(-1, width)
+            view[rows, cols] = view[rows, cols] ^ bits[torch.from_numpy(sel).cuda()]
+        v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                              d_ver.data_ptr(), s)
+        torch.cuda.synchronize()
+        w_host = d_ver.cpu().numpy().view(np.uint32)
+        ok = at2v_mod.unpack_verdicts(w_host, n)
+        assert np.array_equal(np.nonzero(~ok)[0], idx)
+        assert (int(w_host[-1]) >> (n % 32)) == 0, "pad bits of the last verdict word must be 0"
+    finally:
+        v.close()
