@@ -127,9 +127,35 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     gu_add(tt, R3, ca);
     gu_p1p1_to_p2(R2, tt);
   }
+  // The digit words live in a private array that LLVM keeps in scratch: a uniform-index read is a scratch load with an
+  // SGPR offset. Read at the start of the window that needs them, their round trip (together with the pacing load
+  // issued just before) stalled every window on s_waitcnt vmcnt(0) (SQ_WAIT_ANY 12.8% of wave cycles, profiles/r02q).
+  // AT2V_DIGIT_AHEAD=1: the words of the NEXT window's A/R digits and this window's B digits are loaded at the window
+  // start, before the LDS-DMA prefetches (vmcnt counts in issue order, so waiting for them never waits for the
+  // prefetches), and first used a window (A/R) or four doublings (B) later. 0 = the old placement (A/B).
+#ifndef AT2V_DIGIT_AHEAD
+#define AT2V_DIGIT_AHEAD 1
+#endif
+#if AT2V_DIGIT_AHEAD
+  uint32_t wa = sel8(c0d, (nw - 2) >> 3), wr = sel8(c1d, (nw - 2) >> 3);
+#endif
   for (int i = nw - 2; i >= 0; --i) {
+    const bool bwin = (i & 3) == 0 && i < 32;
+    int e0 = 0, e1 = 0;
+#if AT2V_DIGIT_AHEAD
+    // before the pacing store/load of this window: the wait for wa/wr must not wait for them
+    const int da = (int)((wa >> (4 * (i & 7))) & 15) - 7, dr = (int)((wr >> (4 * (i & 7))) & 15) - 7;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"v"(da), "v"(dr) : "memory");  // da, dr exist before the pacing store below is issued
+#endif
+    pace.window();
+    wa = sel8(c0d, (i - 1) >> 3);  // i = 0: index -1 selects word 0, unused
+    wr = sel8(c1d, (i - 1) >> 3);
+    const uint32_t wt0 = sel8(td, i >> 3), wt1 = sel8(td, 4 + (i >> 3));  // used only when bwin (i < 32)
+#else
     pace.window();
     const int da = digit4(c0d, i), dr = digit4(c1d, i);
+#endif
     ta.prefetch(da < 0 ? -da : da);  // both land while the window's four doublings run
     tr.prefetch(dr < 0 ? -dr : dr);
     for (int r = 0; r < 3; ++r) {
@@ -139,11 +165,14 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     gu_p2_dbl(tt, R2);
     gu_p1p1_to_p3(R3, tt);
     pace.mid();
-    const bool bwin = (i & 3) == 0 && i < 32;
-    int e0 = 0, e1 = 0;
     if (bwin) {  // -t digits j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B)
+#if AT2V_DIGIT_AHEAD
+      e0 = (1 << 15) - (int)((wt0 >> (16 * ((i >> 2) & 1))) & 0xffff);
+      e1 = (1 << 15) - (int)((wt1 >> (16 * ((i >> 2) & 1))) & 0xffff);
+#else
       e0 = (1 << 15) - (int)((sel8(td, i >> 3) >> (16 * ((i >> 2) & 1))) & 0xffff);
       e1 = (1 << 15) - (int)((sel8(td, 4 + (i >> 3)) >> (16 * ((i >> 2) & 1))) & 0xffff);
+#endif
     }
     ta.load_prefetched(ca);
     if (bwin) tb0.prefetch(e0 < 0 ? -e0 : e0);  // into A's stage, now consumed
