@@ -72,6 +72,17 @@ constexpr int kNumBtabs = 1;
 #endif
 constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
 
+// A value the compiler cannot prove wave-uniform but that is (the wave index in the block): as an SGPR, the LDS-DMA
+// destinations (M0) need no v_readfirstlane per load. AT2V_WIB_UNIFORM=0: plain VGPR (A/B).
+#ifndef AT2V_WIB_UNIFORM
+#define AT2V_WIB_UNIFORM 1
+#endif
+#if AT2V_WIB_UNIFORM
+#define AT2V_UNIFORM(x) __builtin_amdgcn_readfirstlane(x)
+#else
+#define AT2V_UNIFORM(x) (x)
+#endif
+
 // Per-lane table [0..8](-A) in global scratch. Layout: lane-contiguous, 9 entries x 160 B per lane
 // (1440 B), so the 10 16-byte loads of one entry hit the same 2 cache lines per lane (L1-resident
 // across the 10 loads) whatever entry index each lane selects. (r01 interleaved lanes per 16-byte
@@ -273,7 +284,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
+  const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t nchunks = (n + 63) / 64;
@@ -374,7 +385,7 @@ __global__ __launch_bounds__(kPairBlock, 1) void verify_pair_kernel(
   __shared__ int4 pstage[kPairWaves * 10 * 64];
   __shared__ int4 bstage[kPairWaves * 10 * 64];
   const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
+  const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const int side = lane & 1;
   const uint32_t wave = blockIdx.x * kPairWaves + wib;
   const uint32_t nwaves = gridDim.x * kPairWaves;
