@@ -92,6 +92,9 @@ struct DevTabA {
   int4* base;   // this lane's 1440-byte slot (global)
   int4* stage;  // this wave's 10 x 1 KiB LDS staging buffer for the prefetched entry
   int lane;
+#ifdef AT2V_WAIT_PROBE
+  mutable unsigned long long waited = 0;
+#endif
   template <class Cached>
   __device__ AT2V_INLINE void store(int e, const Cached& c) const {
     static_assert(sizeof(Cached) == 160, "cached point: 40 words");
@@ -122,7 +125,7 @@ struct DevTabA {
   template <class Cached>
   __device__ AT2V_INLINE void load_prefetched(Cached& c) const {
     static_assert(sizeof(Cached) == 160, "cached point: 40 words");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AT2V_PROBE(waited, asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
     int32_t* w = reinterpret_cast<int32_t*>(&c);
 #pragma unroll
     for (int q = 0; q < 10; ++q) {
@@ -163,6 +166,9 @@ struct DevTabB {
   const int4* base;
   int4* stage;  // this wave's 8 x 1 KiB LDS staging buffer
   int lane;
+#ifdef AT2V_WAIT_PROBE
+  mutable unsigned long long waited = 0;
+#endif
   __device__ AT2V_INLINE void prefetch(int e) const {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage may be shared with a just-read entry
 #pragma unroll
@@ -173,7 +179,7 @@ struct DevTabB {
   template <class Niels>
   __device__ AT2V_INLINE void load_prefetched(Niels& n) const {
     static_assert(sizeof(Niels) == 120, "Niels point: 30 words");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AT2V_PROBE(waited, asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
     int32_t w[32];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -256,6 +262,9 @@ struct Pace {
   uint32_t prog;
   uint32_t mate_prog;
   int lag;  // 0 for waves 0..3; AT2V_FAIR_LAG for waves 4..7 (their target lead is negative)
+#ifdef AT2V_WAIT_PROBE
+  unsigned long long probe[4] = {0, 0, 0, 0};  // digit reads, mid-window mark, chunk total, chunk-start loads
+#endif
 #if AT2V_FAIR_LAG >= 0
   __device__ AT2V_INLINE void mark(uint32_t units) { step(2 * units); }
   __device__ AT2V_INLINE void window() { step(1); }
@@ -316,6 +325,9 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
                                             : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
   for (uint32_t c = c_first; c < nchunks;) {
     AT2V_PHASE(0);
+#ifdef AT2V_WAIT_PROBE
+    const unsigned long long t_chunk0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t i = c * 64 + lane;
     const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
     uint32_t Rw[8], Sw[8], Aw[8];
@@ -345,6 +357,12 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
 #endif
     const uint64_t mask = __ballot(good);
+#ifdef AT2V_WAIT_PROBE
+    AT2V_WAIT_PROBE_SINK(ta.waited + tr.waited, tb0.waited + tb1.waited, pace.probe[0], pace.probe[1],
+                         __builtin_amdgcn_s_memtime() - t_chunk0);
+    ta.waited = tr.waited = tb0.waited = tb1.waited = 0;
+    pace.probe[0] = pace.probe[1] = 0;
+#endif
     uint32_t ticket = 0;
     if (lane == 0) {
       verdicts[2 * c] = (uint32_t)mask;

@@ -24,6 +24,18 @@
 #ifndef AT2V_PHASE
 #define AT2V_PHASE(k)
 #endif
+// s_waitcnt probe (tools/phase_bench built with -DAT2V_WAIT_PROBE): `acc += s_memtime cycles spent in stmt`; acc is a
+// member of a kernel-scope object (a table or the pacer), so it stays in registers. Product builds: just stmt.
+#if defined(AT2V_WAIT_PROBE) && defined(__HIP_DEVICE_COMPILE__)
+#define AT2V_PROBE(acc, stmt)                                   \
+  do {                                                          \
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime(); \
+    stmt;                                                       \
+    (acc) += __builtin_amdgcn_s_memtime() - t0_;                \
+  } while (0)
+#else
+#define AT2V_PROBE(acc, stmt) stmt
+#endif
 
 namespace at2v {
 

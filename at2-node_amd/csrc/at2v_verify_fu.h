@@ -144,10 +144,14 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     int e0 = 0, e1 = 0;
 #if AT2V_DIGIT_AHEAD
     // before the pacing store/load of this window: the wait for wa/wr must not wait for them
-    const int da = (int)((wa >> (4 * (i & 7))) & 15) - 7, dr = (int)((wr >> (4 * (i & 7))) & 15) - 7;
+    int da, dr;
+    AT2V_PROBE(pace.probe[0], {
+      da = (int)((wa >> (4 * (i & 7))) & 15) - 7;
+      dr = (int)((wr >> (4 * (i & 7))) & 15) - 7;
 #if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" ::"v"(da), "v"(dr) : "memory");  // da, dr exist before the pacing store below is issued
+      asm volatile("" ::"v"(da), "v"(dr) : "memory");  // da, dr exist before the pacing store below is issued
 #endif
+    });
     pace.window();
     wa = sel8(c0d, (i - 1) >> 3);  // i = 0: index -1 selects word 0, unused
     wr = sel8(c1d, (i - 1) >> 3);
@@ -164,7 +168,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     }
     gu_p2_dbl(tt, R2);
     gu_p1p1_to_p3(R3, tt);
-    pace.mid();
+    AT2V_PROBE(pace.probe[1], pace.mid());
     if (bwin) {  // -t digits j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B)
 #if AT2V_DIGIT_AHEAD
       e0 = (1 << 15) - (int)((wt0 >> (16 * ((i >> 2) & 1))) & 0xffff);

@@ -30,7 +30,24 @@ __device__ __forceinline__ void at2v_phase_mark(int k) {
     at2v_phase_last[w] = t;
   }
 }
+#ifdef AT2V_WAIT_PROBE
+// s_waitcnt probe build (no phase marks, so no extra memory operations in the measured waves): per-chunk sums of the
+// cycles spent in the A/R entry waits, the B entry waits, the digit-word reads and the mid-window pacing mark, and
+// the chunk's total, summed over all chunks
+__device__ unsigned long long at2v_probe_acc[5];
+#define AT2V_WAIT_PROBE_SINK(a, b, c, d, e)       \
+  do {                                           \
+    if ((threadIdx.x & 63) == 0) {               \
+      atomicAdd(&at2v_probe_acc[0], (a));        \
+      atomicAdd(&at2v_probe_acc[1], (b));        \
+      atomicAdd(&at2v_probe_acc[2], (c));        \
+      atomicAdd(&at2v_probe_acc[3], (d));        \
+      atomicAdd(&at2v_probe_acc[4], (e));        \
+    }                                            \
+  } while (0)
+#else
 #define AT2V_PHASE(k) at2v_phase_mark(k)
+#endif
 
 #include "at2v_kernels.hip"
 
@@ -75,6 +92,9 @@ int main(int argc, char** argv) {
   float ms = 0;
   for (int rep = 0; rep < 2; ++rep) {
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_acc), zero.data(), zero.size() * 8));
+#ifdef AT2V_WAIT_PROBE
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_probe_acc), zero.data(), 5 * 8));
+#endif
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_last), zl.data(), zl.size() * 8));
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_wave_t0), zl.data(), zl.size() * 8));
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_wave_t1), zl.data(), zl.size() * 8));
@@ -111,6 +131,18 @@ int main(int argc, char** argv) {
   for (int k = 0; k < 8; ++k)
     printf("  %-24s %6.2f %%   %10.0f wave-cycles per 64-record chunk\n", names[k], 100 * b[k] / tot, b[k] / chunks);
   printf("  total                    %10.0f wave-cycles per chunk (s_memtime; 2 waves share a SIMD)\n", tot / chunks);
+#ifdef AT2V_WAIT_PROBE
+  {
+    unsigned long long pa[5];
+    CHECK(hipMemcpyFromSymbol(pa, HIP_SYMBOL(at2v_probe_acc), sizeof(pa)));
+    const char* pn[4] = {"A/R entry waits", "B entry waits", "digit-word reads (loop top)", "mid-window pacing mark"};
+    for (int k = 0; k < 4; ++k)
+      printf("  probe %-28s %6.2f %% of chunk time  (%10.0f cycles per chunk)\n", pn[k], 100.0 * pa[k] / pa[4],
+             pa[k] / chunks);
+    printf("  probe chunk total %10.0f cycles per chunk\n", pa[4] / chunks);
+  }
+#endif
+#ifndef AT2V_WAIT_PROBE  // the probe build sets no marks: no per-wave timeline
   {
     std::vector<unsigned long long> t0(AT2V_MAX_WAVES), t1(AT2V_MAX_WAVES);
     CHECK(hipMemcpyFromSymbol(t0.data(), HIP_SYMBOL(at2v_wave_t0), t0.size() * 8));
@@ -137,5 +169,6 @@ int main(int argc, char** argv) {
            (s1 - s0) / 100.0, ends[0] / 100, ends[(size_t)(0.1 * m)] / 100, ends[(size_t)(0.5 * m)] / 100,
            ends[(size_t)(0.9 * m)] / 100, ends[(size_t)(0.99 * m)] / 100, span / 100, life / m / span);
   }
+#endif
   return valid == n ? 0 : 2;
 }
