@@ -93,7 +93,7 @@ struct DevTabA {
   int4* stage;  // this wave's 10 x 1 KiB LDS staging buffer for the prefetched entry
   int lane;
 #ifdef AT2V_WAIT_PROBE
-  mutable unsigned long long waited = 0;
+  mutable unsigned long long waited = 0, lds_waited = 0;
 #endif
   template <class Cached>
   __device__ AT2V_INLINE void store(int e, const Cached& c) const {
@@ -135,6 +135,9 @@ struct DevTabA {
       w[4 * q + 2] = v.z;
       w[4 * q + 3] = v.w;
     }
+#ifdef AT2V_WAIT_PROBE
+    AT2V_PROBE(lds_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));
+#endif
   }
 };
 
@@ -167,7 +170,7 @@ struct DevTabB {
   int4* stage;  // this wave's 8 x 1 KiB LDS staging buffer
   int lane;
 #ifdef AT2V_WAIT_PROBE
-  mutable unsigned long long waited = 0;
+  mutable unsigned long long waited = 0, lds_waited = 0;
 #endif
   __device__ AT2V_INLINE void prefetch(int e) const {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage may be shared with a just-read entry
@@ -336,6 +339,9 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     load8(Aw, pk + (size_t)ii * 32);
     const uint32_t o0 = off[ii];
     const uint32_t len = off[ii + 1] - o0;
+#ifdef AT2V_WAIT_PROBE
+    AT2V_PROBE(pace.probe[2], asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
+#endif
     // message words: a wave whose messages all end >= 8 bytes before the buffer end reads two aligned words and
     // funnel-shifts them (no per-lane branch); otherwise every byte is bounds-checked (the last records of a batch)
     const int msg_fast =
@@ -359,9 +365,9 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     const uint64_t mask = __ballot(good);
 #ifdef AT2V_WAIT_PROBE
     AT2V_WAIT_PROBE_SINK(ta.waited + tr.waited, tb0.waited + tb1.waited, pace.probe[0], pace.probe[1],
-                         __builtin_amdgcn_s_memtime() - t_chunk0);
-    ta.waited = tr.waited = tb0.waited = tb1.waited = 0;
-    pace.probe[0] = pace.probe[1] = 0;
+                         __builtin_amdgcn_s_memtime() - t_chunk0, ta.lds_waited + tr.lds_waited, pace.probe[2]);
+    ta.waited = tr.waited = tb0.waited = tb1.waited = ta.lds_waited = tr.lds_waited = tb0.lds_waited = tb1.lds_waited = 0;
+    pace.probe[0] = pace.probe[1] = pace.probe[2] = 0;
 #endif
     uint32_t ticket = 0;
     if (lane == 0) {

@@ -34,8 +34,8 @@ __device__ __forceinline__ void at2v_phase_mark(int k) {
 // s_waitcnt probe build (no phase marks, so no extra memory operations in the measured waves): per-chunk sums of the
 // cycles spent in the A/R entry waits, the B entry waits, the digit-word reads and the mid-window pacing mark, and
 // the chunk's total, summed over all chunks
-__device__ unsigned long long at2v_probe_acc[5];
-#define AT2V_WAIT_PROBE_SINK(a, b, c, d, e)       \
+__device__ unsigned long long at2v_probe_acc[7];
+#define AT2V_WAIT_PROBE_SINK(a, b, c, d, e, f, g) \
   do {                                           \
     if ((threadIdx.x & 63) == 0) {               \
       atomicAdd(&at2v_probe_acc[0], (a));        \
@@ -43,6 +43,8 @@ __device__ unsigned long long at2v_probe_acc[5];
       atomicAdd(&at2v_probe_acc[2], (c));        \
       atomicAdd(&at2v_probe_acc[3], (d));        \
       atomicAdd(&at2v_probe_acc[4], (e));        \
+      atomicAdd(&at2v_probe_acc[5], (f));        \
+      atomicAdd(&at2v_probe_acc[6], (g));        \
     }                                            \
   } while (0)
 #else
@@ -93,7 +95,7 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 2; ++rep) {
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_acc), zero.data(), zero.size() * 8));
 #ifdef AT2V_WAIT_PROBE
-    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_probe_acc), zero.data(), 5 * 8));
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_probe_acc), zero.data(), 7 * 8));
 #endif
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_phase_last), zl.data(), zl.size() * 8));
     CHECK(hipMemcpyToSymbol(HIP_SYMBOL(at2v_wave_t0), zl.data(), zl.size() * 8));
@@ -133,12 +135,15 @@ int main(int argc, char** argv) {
   printf("  total                    %10.0f wave-cycles per chunk (s_memtime; 2 waves share a SIMD)\n", tot / chunks);
 #ifdef AT2V_WAIT_PROBE
   {
-    unsigned long long pa[5];
+    unsigned long long pa[7];
     CHECK(hipMemcpyFromSymbol(pa, HIP_SYMBOL(at2v_probe_acc), sizeof(pa)));
-    const char* pn[4] = {"A/R entry waits", "B entry waits", "digit-word reads (loop top)", "mid-window pacing mark"};
-    for (int k = 0; k < 4; ++k)
+    const char* pn[7] = {"A/R entry waits", "B entry waits", "digit-word reads (loop top)", "mid-window pacing mark",
+                         "-", "A/R entry LDS reads (lgkm)", "chunk-start input loads"};
+    for (int k = 0; k < 7; ++k) {
+      if (k == 4) continue;
       printf("  probe %-28s %6.2f %% of chunk time  (%10.0f cycles per chunk)\n", pn[k], 100.0 * pa[k] / pa[4],
              pa[k] / chunks);
+    }
     printf("  probe chunk total %10.0f cycles per chunk\n", pa[4] / chunks);
   }
 #endif
