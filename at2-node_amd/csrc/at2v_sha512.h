@@ -52,9 +52,13 @@ AT2V_HD AT2V_INLINE uint64_t sha_ror(uint64_t x, int n) {
 #if defined(__HIP_DEVICE_COMPILE__) && AT2V_SHA_BITOP3
 template <int LUT>
 __device__ AT2V_INLINE uint64_t sha_bitop3(uint64_t x, uint64_t y, uint64_t z) {
-  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, LUT);
-  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), LUT);
-  return ((uint64_t)hi << 32) | lo;
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 v;
+  v.x = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, LUT);
+  v.y = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), LUT);
+  // a bit cast of the pair, not (hi << 32) | lo: LLVM turns that disjoint OR into an ADD and splits the consuming
+  // 64-bit adds into two zero-padded ones plus register moves
+  return __builtin_bit_cast(uint64_t, v);
 }
 AT2V_HD AT2V_INLINE uint64_t sha_xor3(uint64_t x, uint64_t y, uint64_t z) { return sha_bitop3<0x96>(x, y, z); }
 AT2V_HD AT2V_INLINE uint64_t sha_maj(uint64_t x, uint64_t y, uint64_t z) { return sha_bitop3<0xe8>(x, y, z); }
@@ -62,6 +66,18 @@ AT2V_HD AT2V_INLINE uint64_t sha_maj(uint64_t x, uint64_t y, uint64_t z) { retur
 AT2V_HD AT2V_INLINE uint64_t sha_xor3(uint64_t x, uint64_t y, uint64_t z) { return x ^ y ^ z; }
 AT2V_HD AT2V_INLINE uint64_t sha_maj(uint64_t x, uint64_t y, uint64_t z) { return (x & y) ^ (z & (x ^ y)); }
 #endif
+// (hi << 32) | lo; on the device as a bit cast of the register pair (see sha_bitop3)
+AT2V_HD AT2V_INLINE uint64_t sha_pair(uint32_t lo, uint32_t hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 v;
+  v.x = lo;
+  v.y = hi;
+  return __builtin_bit_cast(uint64_t, v);
+#else
+  return ((uint64_t)hi << 32) | lo;
+#endif
+}
 AT2V_HD AT2V_INLINE uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -158,7 +174,7 @@ AT2V_HD AT2V_INLINE void sha512_prefixed(uint64_t h[8], const uint32_t* prefix, 
         }
         be[half] = bswap32(le);
       }
-      w[t] = ((uint64_t)be[0] << 32) | be[1];
+      w[t] = sha_pair(be[1], be[0]);
     }
     if (b == nblocks - 1) {
       w[14] = 0;
