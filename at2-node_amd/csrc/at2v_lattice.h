@@ -151,6 +151,10 @@ AT2V_HD AT2V_INLINE void euclid_reduce(U256& a, U256& ma, const U256& b, const U
 #define AT2V_LEHMER_IEEE_DIV 0  // 1: IEEE float division in the Lehmer quotient estimate (A/B)
 #endif
 
+#ifndef AT2V_LATTICE_EXACT_MATRIX
+#define AT2V_LATTICE_EXACT_MATRIX 1  // exact Euclid steps through lehmer_apply (0: the separate subtract-and-swap path)
+#endif
+
 #ifndef AT2V_LATTICE_LEHMER
 #define AT2V_LATTICE_LEHMER 2  // 0: plain Euclid, 1: Lehmer on 62-bit leading parts, 2: on 30-bit parts
 #endif
@@ -338,6 +342,27 @@ AT2V_HD AT2V_INLINE void lattice_reduce(HalfScalars& out, const uint32_t k[8]) {
     lehmer_round32(steps, mA, mB, mC, mD, ra, rb, C);
 #else
     lehmer_round(steps, mA, mB, mC, mD, ra, rb, C);
+#endif
+#if AT2V_LATTICE_EXACT_MATRIX
+    if (steps == 0) {
+      // One exact Euclid step as the cofactor matrix (0 1; 1 -q), so it runs through the same lehmer_apply as a
+      // Lehmer round instead of a separate subtract-and-swap path (whose join copied the 4 x 8-word state). The
+      // double quotient is taken only when it is provably the floor: q < 2^31 and the fraction at least 2^-16 away
+      // from an integer (the two 256-bit -> double conversions and the division err by < 2^-48 relative, i.e.
+      // < 2^-17 absolute here); otherwise (probability ~2^-15 per step) the exact path below runs.
+      const double ratio = u256_to_double(ra) / u256_to_double(rb);
+      if (ratio < 2147483648.0) {
+        const double fl = (double)(int64_t)ratio;
+        const double fr = ratio - fl;
+        if (fr > 1.0 / 65536 && fr < 1.0 - 1.0 / 65536) {
+          mA = 0;
+          mB = 1;
+          mC = 1;
+          mD = -(int64_t)fl;
+          steps = 1;
+        }
+      }
+    }
 #endif
     if (steps > 0) {
       lehmer_apply(ra, rb, ma, mb, mA, mB, mC, mD);
