@@ -151,6 +151,10 @@ AT2V_HD AT2V_INLINE void euclid_reduce(U256& a, U256& ma, const U256& b, const U
 #define AT2V_LEHMER_IEEE_DIV 0  // 1: IEEE float division in the Lehmer quotient estimate (A/B)
 #endif
 
+#ifndef AT2V_LATTICE_PINGPONG
+#define AT2V_LATTICE_PINGPONG 1  // two alternating state sets in the reduction loop (0: one set, state copied back)
+#endif
+
 #ifndef AT2V_LATTICE_EXACT_MATRIX
 #define AT2V_LATTICE_EXACT_MATRIX 1  // exact Euclid steps through lehmer_apply (0: the separate subtract-and-swap path)
 #endif
@@ -312,6 +316,49 @@ AT2V_HD AT2V_INLINE void lehmer_apply(U256& ra, U256& rb, U256& ma, U256& mb, in
   mb = xb;
 }
 
+// One reduction round from (ra, rb, ma, mb) into a DIFFERENT set (na, nb, xa, xb): a Lehmer round, an exact step as
+// the matrix (0 1; 1 -q), or (rare) the exact subtract-and-swap step. Writing into the other set lets the caller
+// alternate two register sets (AT2V_LATTICE_PINGPONG) instead of copying the new state back every round.
+AT2V_HD AT2V_INLINE void lattice_step(const U256& ra, const U256& rb, const U256& ma, const U256& mb, U256& na, U256& nb,
+                                      U256& xa, U256& xb, int& idx, const U256& C) {
+  int steps;
+  int64_t mA, mB, mC, mD;
+  lehmer_round32(steps, mA, mB, mC, mD, ra, rb, C);
+  if (steps == 0) {  // exact step through the same apply when the double quotient is provably the floor
+    const double ratio = u256_to_double(ra) / u256_to_double(rb);
+    if (ratio < 2147483648.0) {
+      const double fl = (double)(int64_t)ratio;
+      const double fr = ratio - fl;
+      if (fr > 1.0 / 65536 && fr < 1.0 - 1.0 / 65536) {
+        mA = 0;
+        mB = 1;
+        mC = 1;
+        mD = -(int64_t)fl;
+        steps = 1;
+      }
+    }
+  }
+  if (steps > 0) {
+    u256_lincomb(na, ra, mA, rb, mB);
+    u256_lincomb(nb, ra, mC, rb, mD);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xa.w[i] = xb.w[i] = 0;
+    u256_addmul(xa, ma, (uint32_t)iabs64(mA));
+    u256_addmul(xa, mb, (uint32_t)iabs64(mB));
+    u256_addmul(xb, ma, (uint32_t)iabs64(mC));
+    u256_addmul(xb, mb, (uint32_t)iabs64(mD));
+    idx += steps;
+  } else {
+    U256 r = ra, m = ma;
+    euclid_reduce(r, m, rb, mb);  // r = ra mod rb, m = ma + q mb
+    na = rb;
+    xa = mb;
+    nb = r;
+    xb = m;
+    ++idx;
+  }
+}
+
 struct HalfScalars {
   uint32_t c0[8];   // c0 >= 0
   uint32_t c1[8];   // |c1| (odd)
@@ -334,7 +381,26 @@ AT2V_HD AT2V_INLINE void lattice_reduce(HalfScalars& out, const uint32_t k[8]) {
     mb.w[i] = i == 0;
   }
   int idx = 1;  // rb = r_idx; sign(t_idx) = (-1)^(idx+1)
-#if AT2V_LATTICE_LEHMER
+#if AT2V_LATTICE_LEHMER == 2 && AT2V_LATTICE_PINGPONG
+  {
+    U256 sa, sb, sma, smb;
+    int in_second = 0;
+    for (int guard = 0; guard < 200 && u256_ge(rb, C); ++guard) {
+      lattice_step(ra, rb, ma, mb, sa, sb, sma, smb, idx, C);
+      if (!u256_ge(sb, C)) {
+        in_second = 1;
+        break;
+      }
+      lattice_step(sa, sb, sma, smb, ra, rb, ma, mb, idx, C);
+    }
+    if (in_second) {
+      ra = sa;
+      rb = sb;
+      ma = sma;
+      mb = smb;
+    }
+  }
+#elif AT2V_LATTICE_LEHMER
   for (int guard = 0; guard < 400 && u256_ge(rb, C); ++guard) {
     int steps;
     int64_t mA, mB, mC, mD;
