@@ -29,7 +29,7 @@ _POLICIES = {"dalek": POLICY_DALEK_V1, "dalek_v1": POLICY_DALEK_V1, "libsodium":
              POLICY_LIBSODIUM_1_0_18: POLICY_LIBSODIUM_1_0_18}
 
 # must match include/at2v.h (checked by tests/test_abi.py)
-EXPORTED_SYMBOLS = ("at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
+EXPORTED_SYMBOLS = ("at2v_abi_version", "at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
                     "at2v_verify_one", "at2v_verify_one_policy", "at2v_strerror", "at2v_gen_records_device",
                     "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
                     "at2v_comm_get_unique_id", "at2v_comm_init_rank", "at2v_verify_shard_gather_device",
@@ -52,9 +52,13 @@ class VerifyError(Exception):
     """Signature rejected (drop::crypto::sign::VerifyError)."""
 
 
+ABI_VERSION = 3  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
+E_PEER = -7      # AT2V_E_PEER: another rank of the communicator failed this collective batch
+
+
 class _Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int),
-                ("small_batch_max", ctypes.c_uint32)]
+                ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32)]
 
 
 SMALL_BATCH_DEFAULT = 32768     # include/at2v.h AT2V_SMALL_BATCH_DEFAULT
@@ -64,7 +68,7 @@ SMALL_BATCH_OFF = 0xFFFFFFFF    # include/at2v.h AT2V_SMALL_BATCH_OFF: never use
 class _Info(ctypes.Structure):
     _fields_ = [("num_gpus", ctypes.c_int), ("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
                 ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int), ("vgprs", ctypes.c_int),
-                ("rank", ctypes.c_int), ("world", ctypes.c_int)]
+                ("rank", ctypes.c_int), ("world", ctypes.c_int), ("gathers", ctypes.c_uint64)]
 
 
 UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)
@@ -88,6 +92,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
+    lib.at2v_abi_version.argtypes = []
+    lib.at2v_abi_version.restype = ctypes.c_int
+    if lib.at2v_abi_version() != ABI_VERSION:  # the structs below would not match the library's
+        raise At2vError(-1, f"{path} has ABI version {lib.at2v_abi_version()}, this binding needs {ABI_VERSION}")
     P, u8p, u32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32)
     lib.at2v_create.argtypes = [ctypes.POINTER(_Opts), ctypes.POINTER(P)]
     lib.at2v_create.restype = ctypes.c_int
@@ -165,12 +173,14 @@ def pack_records(pks: Sequence[bytes], sigs: Sequence[bytes], msgs: Sequence[byt
 class BatchVerifier:
     """Owns an at2v context (one or more gfx950 devices)."""
 
-    def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek", small_batch_max: int = 0):
+    def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek", small_batch_max: int = 0,
+                 sender_cache: int = 0):
         """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
-        0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel."""
+        0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel.
+        sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off)."""
         self._lib = load_library()
         self.policy = _POLICIES[policy]
-        opts = _Opts(device, num_gpus, self.policy, small_batch_max)
+        opts = _Opts(device, num_gpus, self.policy, small_batch_max, sender_cache)
         h = ctypes.c_void_p()
         _check(self._lib.at2v_create(ctypes.byref(opts), ctypes.byref(h)), "at2v_create")
         self._h = h

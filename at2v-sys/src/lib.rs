@@ -29,6 +29,10 @@ pub struct At2vLedger {
     _private: [u8; 0],
 }
 
+/// include/at2v.h AT2V_ABI_VERSION: the layouts of the #[repr(C)] structs below. `BatchVerifier::new` and
+/// `Queue::new` refuse a library that reports another version (the structs are copied whole by the library).
+pub const AT2V_ABI_VERSION: c_int = 3;
+
 pub const AT2V_POLICY_DALEK_V1: c_int = 0;
 pub const AT2V_POLICY_LIBSODIUM_1_0_18: c_int = 1;
 
@@ -39,6 +43,7 @@ pub const AT2V_E_HIP: c_int = -3;
 pub const AT2V_E_OOM: c_int = -4;
 pub const AT2V_E_ALIGN: c_int = -5;
 pub const AT2V_E_RCCL: c_int = -6;
+pub const AT2V_E_PEER: c_int = -7;
 
 pub const AT2V_UNIQUE_ID_BYTES: usize = 128;
 
@@ -62,14 +67,17 @@ pub const AT2V_VERDICT_INVALID: u8 = 0;
 pub const AT2V_VERDICT_VALID: u8 = 1;
 pub const AT2V_VERDICT_FAILED: u8 = 0xff;
 
+/// `Default`: device 0, one GPU, DALEK_V1, library-default small-batch threshold, no sender cache.
 #[repr(C)]
-#[derive(Clone, Copy, Debug)]
+#[derive(Clone, Copy, Debug, Default)]
 pub struct At2vOpts {
     pub device: c_int,
     pub num_gpus: c_int,
     pub policy: c_int,
     /// launches of at most this many records run the low-latency kernel; 0 = 32768, AT2V_SMALL_BATCH_OFF = never
     pub small_batch_max: u32,
+    /// per-sender A cache capacity in distinct public keys; 0 = off
+    pub sender_cache: u32,
 }
 
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
@@ -86,10 +94,12 @@ pub struct At2vInfo {
     pub vgprs: c_int,
     pub rank: c_int,
     pub world: c_int,
+    pub gathers: u64,
 }
 
+/// `Default`: device 0, DALEK_V1, and the library defaults for every size (65536 records, 1 ms, 256 B, depth 3).
 #[repr(C)]
-#[derive(Clone, Copy, Debug)]
+#[derive(Clone, Copy, Debug, Default)]
 pub struct At2vQueueOpts {
     pub device: c_int,
     pub policy: c_int,
@@ -154,6 +164,7 @@ pub struct At2vApplyStats {
 // ---------------------------------------------------------------- functions (at2v.h, same order)
 
 extern "C" {
+    pub fn at2v_abi_version() -> c_int;
     pub fn at2v_create(opts: *const At2vOpts, out: *mut *mut At2vCtx) -> c_int;
     pub fn at2v_destroy(ctx: *mut At2vCtx);
     pub fn at2v_verify_batch(ctx: *mut At2vCtx, pk: *const u8, sig: *const u8, msg: *const u8, msg_off: *const u32,
@@ -240,6 +251,13 @@ pub fn verify_one(public_key: &[u8; 32], signature: &[u8; 64], message: &[u8]) -
     check(unsafe { at2v_verify_one(public_key.as_ptr(), signature.as_ptr(), m, message.len()) }).map(|v| v == 1)
 }
 
+fn check_abi() -> Result<(), Error> {
+    if unsafe { at2v_abi_version() } != AT2V_ABI_VERSION {
+        return Err(Error(AT2V_E_INVALID));
+    }
+    Ok(())
+}
+
 /// Owner of an at2v context (GPU). Not Sync: one thread at a time; call from `spawn_blocking` or a
 /// dedicated thread, never on an async executor thread.
 pub struct BatchVerifier(*mut At2vCtx);
@@ -247,11 +265,16 @@ pub struct BatchVerifier(*mut At2vCtx);
 unsafe impl Send for BatchVerifier {}
 
 impl BatchVerifier {
-    pub fn new(device: i32, num_gpus: i32, policy: c_int) -> Result<Self, Error> {
-        let opts = At2vOpts { device, num_gpus, policy };
+    pub fn new(opts: &At2vOpts) -> Result<Self, Error> {
+        check_abi()?;
         let mut p = std::ptr::null_mut();
-        check(unsafe { at2v_create(&opts, &mut p) })?;
+        check(unsafe { at2v_create(opts, &mut p) })?;
         Ok(BatchVerifier(p))
+    }
+
+    /// `num_gpus` devices from `device` on, library defaults otherwise.
+    pub fn on_devices(device: i32, num_gpus: i32, policy: c_int) -> Result<Self, Error> {
+        Self::new(&At2vOpts { device, num_gpus, policy, ..Default::default() })
     }
 
     /// One process per GPU: join the node's RCCL communicator (collective over `world` ranks).
@@ -261,7 +284,7 @@ impl BatchVerifier {
 
     /// Records in the at2v_verify_batch layout -> one bool per record (bit i of the verdict bitmap).
     /// `sharded`: every rank passes the same node batch; each verifies its range and the RCCL all-gather
-    /// returns the whole bitmap (requires `init_rank`).
+    /// returns the whole bitmap (requires `init_rank`). Err(AT2V_E_PEER): another rank failed; discard the batch.
     pub fn verify(&mut self, pk: &[u8], sig: &[u8], msg: &[u8], msg_off: &[u32], sharded: bool)
                   -> Result<Vec<bool>, Error> {
         let n = msg_off.len().saturating_sub(1);
@@ -281,11 +304,95 @@ impl BatchVerifier {
         check(rc)?;
         Ok((0..n).map(|i| (words[i / 32] >> (i % 32)) & 1 == 1).collect())
     }
+
+    /// Device-resident records (the layout of `verify`, in HBM of the context's first device), asynchronous on
+    /// `hip_stream` (a hipStream_t; null = the null stream): the verdict words are valid once the stream has
+    /// reached this point.
+    ///
+    /// # Safety
+    /// Every pointer must be a device allocation of the context's device with the sizes of include/at2v.h
+    /// (`d_pk` n x 32 B and `d_sig` n x 64 B, 16-byte aligned; `d_msg_off` n + 1 offsets into `msg_bytes` bytes at
+    /// `d_msg`; `d_verdicts` ceil(n/32) words) and stay alive until the stream has passed the launch.
+    pub unsafe fn verify_device(&mut self, d_pk: *const u8, d_sig: *const u8, d_msg: *const u8, msg_bytes: usize,
+                                d_msg_off: *const u32, n: usize, d_verdicts: *mut u32, hip_stream: *mut c_void)
+                                -> Result<(), Error> {
+        check(at2v_verify_batch_device(self.0, d_pk, d_sig, d_msg, msg_bytes, d_msg_off, n, d_verdicts, hip_stream))
+            .map(|_| ())
+    }
+
+    pub fn info(&self) -> Result<At2vInfo, Error> {
+        let mut i = At2vInfo::default();
+        check(unsafe { at2v_get_info(self.0, &mut i) })?;
+        Ok(i)
+    }
 }
 
 impl Drop for BatchVerifier {
     fn drop(&mut self) {
         unsafe { at2v_destroy(self.0) }
+    }
+}
+
+/// The server's verify call site: payloads go in with `submit`, verdicts come back from `poll`
+/// in submission (ticket) order. Thread-safe on the library side (any number of producers, poll from any thread).
+pub struct Queue(*mut At2vQueue);
+
+unsafe impl Send for Queue {}
+unsafe impl Sync for Queue {}
+
+/// One polled verdict: `Some(true)` valid, `Some(false)` invalid, `None` the batch failed on the device
+/// (re-submit; it is neither valid nor invalid).
+pub type Verdict = Option<bool>;
+
+impl Queue {
+    pub fn new(opts: &At2vQueueOpts) -> Result<Self, Error> {
+        check_abi()?;
+        let mut p = std::ptr::null_mut();
+        check(unsafe { at2v_queue_create(opts, &mut p) })?;
+        Ok(Queue(p))
+    }
+
+    /// Records in the at2v_verify_batch layout; returns the ticket of the first (the rest follow consecutively).
+    /// Blocks only while every batch slot is in flight (backpressure).
+    pub fn submit(&self, pk: &[u8], sig: &[u8], msg: &[u8], msg_off: &[u32]) -> Result<u64, Error> {
+        let n = msg_off.len().saturating_sub(1);
+        if pk.len() != 32 * n || sig.len() != 64 * n {
+            return Err(Error(AT2V_E_INVALID));
+        }
+        let m = if msg.is_empty() { std::ptr::null() } else { msg.as_ptr() };
+        let mut first = 0u64;
+        check(unsafe { at2v_queue_submit(self.0, pk.as_ptr(), sig.as_ptr(), m, msg_off.as_ptr(), n, &mut first) })?;
+        Ok(first)
+    }
+
+    pub fn flush(&self) -> Result<(), Error> {
+        check(unsafe { at2v_queue_flush(self.0) }).map(|_| ())
+    }
+
+    /// Up to `max` completed (ticket, verdict) pairs in ticket order, waiting up to `timeout_us` for the first.
+    pub fn poll(&self, max: usize, timeout_us: u32) -> Result<Vec<(u64, Verdict)>, Error> {
+        let mut t = vec![0u64; max];
+        let mut v = vec![0u8; max];
+        let k = unsafe { at2v_queue_poll(self.0, t.as_mut_ptr(), v.as_mut_ptr(), max, timeout_us) };
+        if k < 0 {
+            return Err(Error(k as c_int));
+        }
+        Ok((0..k as usize)
+            .map(|i| (t[i], match v[i] { AT2V_VERDICT_VALID => Some(true), AT2V_VERDICT_INVALID => Some(false), _ => None }))
+            .collect())
+    }
+
+    pub fn stats(&self) -> Result<At2vQueueStats, Error> {
+        let mut s = At2vQueueStats::default();
+        check(unsafe { at2v_queue_get_stats(self.0, &mut s) })?;
+        Ok(s)
+    }
+}
+
+impl Drop for Queue {
+    /// Seals and completes everything submitted, then frees.
+    fn drop(&mut self) {
+        unsafe { at2v_queue_destroy(self.0) }
     }
 }
 

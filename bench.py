@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--e2e", type=int, default=1, help="1 = also time the host-buffer path (H2D + verify + D2H)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only (tests): the launcher and gloo control plane with oracle verdicts, no GPU")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds a rank waits in the gloo rendezvous / barriers before giving up (N > 1)")
     ap.add_argument("--pmc-traffic", type=int, default=1,
                     help="1 = at N=1, measure HBM-side bytes per verify launch with two rocprofv3 PMC passes "
                          "(FETCH_SIZE, WRITE_SIZE) of a 2-step child run; 0 = skip (roofline.traffic null)")
@@ -72,8 +74,11 @@ def _free_port():
 def self_launch(args):
     """`bench.py --gpus N` (N > 1) outside torch.distributed.run: start N rank processes of this script (one per
     GPU) as children, before this process touches any GPU, and pass rank 0's JSON line through. Children, never
-    exec: the parent stays a plain process and exits with the worst child status."""
+    exec: the parent stays a plain process. It watches EVERY child: on the first non-zero exit it stops the other
+    ranks (SIGTERM, then SIGKILL after 10 s; by their PIDs) and exits with that status, so a rank that dies early
+    cannot leave the others blocked in the gloo rendezvous or inside an RCCL collective until the driver's limit."""
     import subprocess
+    import threading
     port = _free_port()
     procs = []
     for r in range(args.gpus):
@@ -81,11 +86,37 @@ def self_launch(args):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
-    out = procs[0].communicate()[0]
-    rcs = [p.wait() for p in procs]
-    sys.stdout.write(out.decode())
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = None
+    while failed is None:
+        rcs = [p.poll() for p in procs]
+        bad = [(r, rc) for r, rc in enumerate(rcs) if rc not in (None, 0)]
+        if bad:
+            failed = bad[0]
+        elif all(rc == 0 for rc in rcs):
+            break
+        else:
+            time.sleep(0.2)
+    if failed is not None:
+        sys.stderr.write(f"bench.py: rank {failed[0]} exited with status {failed[1]}; stopping the other ranks\n")
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reader.join(timeout=10)
+    sys.stdout.write(b"".join(out).decode())
     sys.stdout.flush()
-    return max(abs(rc) for rc in rcs)
+    if failed is not None:
+        return abs(failed[1]) or 1
+    return 0
 
 
 def usable_cores():
@@ -135,8 +166,13 @@ def main():
     # control plane: the RCCL unique id, barriers and the MAX/MIN reductions of timings and checks. Under
     # torch.distributed.run at N = 1 the same path runs with world 1, so a one-GPU box rehearses it.
     use_dist = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    fail_rank = os.environ.get("AT2V_BENCH_FAIL_RANK")  # failure injection (tests/test_bench_launch.py)
+    if fail_rank is not None and int(fail_rank) == rank:
+        raise SystemExit(f"rank {rank}: injected failure (AT2V_BENCH_FAIL_RANK)")
     if use_dist:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.dist_timeout))
     if args.dry_run:
         out = dry_run(args, rank, world, use_dist, dist, torch, np)
         if rank == 0:
@@ -260,8 +296,11 @@ def main():
                 "traffic": None,
                 "alg_macs_per_verify": MAC_PER_VERIFY,
                 "alg_bytes_per_verify": 32 + 64 + L + 4,
-                "hbm_gbs": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9,
-                "hbm_frac": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9 / HBM_PEAK_GBS,
+                # algorithmic input rate (records x 200 B / kernel time); the measured memory-side rate from the
+                # PMC counters is hbm_gbs (filled below at N = 1 when the counter passes run)
+                "alg_input_gbs": per_gpu_kernel_rate * (32 + 64 + L + 4) / 1e9,
+                "hbm_gbs": None,
+                "hbm_frac": None,
             },
         }
         if e2e:
@@ -273,6 +312,10 @@ def main():
         if tr is not None:
             out["roofline"]["traffic"] = tr["bytes_per_launch"]
             out["roofline"]["traffic_detail"] = tr
+            # memory-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, L2's fabric side: MALL hits included, so an
+            # upper bound on HBM bytes) over the un-profiled kernel time of this run
+            out["roofline"]["hbm_gbs"] = tr["bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
+            out["roofline"]["hbm_frac"] = out["roofline"]["hbm_gbs"] / HBM_PEAK_GBS
         vl = pmc_valu(args, n, L)
         if vl is not None:
             out["roofline"]["valu_measured"] = vl

@@ -25,6 +25,13 @@
 extern "C" {
 #endif
 
+/* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
+ * version 3 appended at2v_opts.sender_cache and at2v_info.gathers and the AT2V_E_PEER code (version 2 appended
+ * at2v_opts.small_batch_max and at2v_queue_opts.flags). A binding checks at2v_abi_version() == AT2V_ABI_VERSION
+ * before passing any struct (the Python and Rust bindings in this repo refuse a mismatching library). */
+#define AT2V_ABI_VERSION 3
+int at2v_abi_version(void);
+
 typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, and the RCCL
                                      communicator once at2v_comm_init_rank has attached one */
 
@@ -39,6 +46,10 @@ typedef struct {
   at2v_policy policy; /* verdict semantics */
   uint32_t small_batch_max; /* launches of at most this many records run the low-latency kernel (two lanes per
                                record, one wave per SIMD); 0 = 32768; AT2V_SMALL_BATCH_OFF = never */
+  uint32_t sender_cache;    /* per-sender A cache (AT2 senders repeat: accounts/account.rs:36-43): capacity in distinct
+                               public keys, 0 = off. A record whose sender A is cached skips decoding A and building
+                               its [j]A table; the verdict is unchanged (the cache holds only values derived from the
+                               32 bytes of A, and every hit is confirmed by comparing those bytes). */
 } at2v_opts;
 #define AT2V_SMALL_BATCH_DEFAULT 32768u
 #define AT2V_SMALL_BATCH_OFF 0xffffffffu
@@ -50,7 +61,9 @@ enum {
   AT2V_E_HIP = -3,      /* HIP runtime error */
   AT2V_E_OOM = -4,      /* device or host allocation failed */
   AT2V_E_ALIGN = -5,    /* device pointer not 16-byte aligned (pk, sig) or 4-byte aligned (offsets, verdicts) */
-  AT2V_E_RCCL = -6      /* RCCL communicator / collective failure (at2v_comm_init_rank, the verdict all-gather) */
+  AT2V_E_RCCL = -6,     /* RCCL communicator / collective failure (at2v_comm_init_rank, the verdict all-gather) */
+  AT2V_E_PEER = -7      /* at2v_verify_batch_sharded / at2v_comm_init_rank: this rank succeeded but another rank of the
+                           communicator failed; that rank's records are verdict 0 (fail closed), discard the batch */
 };
 
 /* Create / destroy a context. opts may be NULL (device 0, one GPU, DALEK_V1). Replaces nothing in the
@@ -122,6 +135,7 @@ typedef struct {
   int vgprs;           /* VGPRs per lane of the verify kernel (from the code object) */
   int rank;            /* at2v_comm_init_rank: this context's rank, else 0 */
   int world;           /* at2v_comm_init_rank: ranks in the communicator, else 0 */
+  uint64_t gathers;    /* verdict all-gathers this context has issued (failure paths included) */
 } at2v_info;
 int at2v_get_info(at2v_ctx* ctx, at2v_info* out);
 
@@ -133,17 +147,28 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out);
 #define AT2V_UNIQUE_ID_BYTES 128
 int at2v_comm_get_unique_id(uint8_t out[AT2V_UNIQUE_ID_BYTES]);
 /* Attach an RCCL communicator on ctx's device (single-device contexts only). Collective: blocks until all
- * `world` ranks have called it. */
+ * `world` ranks have called it. The ranks agree on the outcome: if any rank fails its local set-up, every rank
+ * returns an error (AT2V_E_PEER on the ranks that did not fail themselves) and no communicator is attached.
+ *
+ * Failure model of the collective calls below (no rank is ever left waiting inside a collective for a rank that
+ * returned early): argument errors are decided from inputs every rank shares (the whole node batch, words_per_rank),
+ * so all ranks return before any collective or none does; any later, rank-local failure (allocation, upload, launch)
+ * makes that rank join the all-gather anyway with zero verdict words, so its records are verdict 0 on every rank. A
+ * device that stops executing work altogether cannot be hidden from its peers. */
 int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BYTES], int rank, int world);
 /* Device buffers, asynchronous on hip_stream: verify this rank's n_local records (<= 32*words_per_rank) into
  * d_bitmap + rank*words_per_rank (pad words zeroed), then all-gather (in place) so d_bitmap holds
- * world*words_per_rank words on every rank. Collective: every rank calls it with the same words_per_rank. */
+ * world*words_per_rank words on every rank. Collective: every rank calls it with the same words_per_rank and a
+ * valid 4-byte-aligned d_bitmap (AT2V_E_INVALID / AT2V_E_ALIGN otherwise, before the collective). Any other error
+ * of this rank (bad record pointers, misalignment, launch failure) is returned AFTER it has joined the all-gather
+ * with a zero slice. */
 int at2v_verify_shard_gather_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                                     size_t msg_bytes, const uint32_t* d_msg_off, size_t n_local,
                                     size_t words_per_rank, uint32_t* d_bitmap, void* hip_stream);
 /* Host buffers, synchronous: every rank passes the SAME node batch (at2v_verify_batch layout); each uploads
  * and verifies only its own range, the all-gather fills in the rest, and every rank receives all ceil(n/32)
- * verdict words in record order. Collective. */
+ * verdict words in record order. Collective. Every rank returns AT2V_OK only if every rank succeeded; otherwise the
+ * failing rank returns its error and the others AT2V_E_PEER. */
 int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                               const uint32_t* msg_off, size_t n, uint32_t* verdicts);
 

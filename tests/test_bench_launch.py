@@ -24,3 +24,21 @@ def test_bench_self_launch_dry_run(gpus):
     r = json.loads(lines[0])
     assert r["dry_run"] and r["n_gpus"] == gpus and r["verdict_match"] == 1.0 and r["unique_id_shared"]
     assert 0 < r["valid"] < r["records"]
+
+
+@pytest.mark.parametrize("fail_rank", [1, 0])
+def test_bench_self_launch_stops_all_ranks_when_one_dies(fail_rank):
+    """a rank that exits early (here before the gloo rendezvous, so its peers would block in it)
+    makes the launcher stop the other ranks and exit non-zero within seconds, not at the driver's time limit."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID")}
+    env["AT2V_BENCH_FAIL_RANK"] = str(fail_rank)
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--dry-run",
+                          "--records-per-gpu", "1000"], capture_output=True, text=True, timeout=120, env=env)
+    dt = time.time() - t0
+    assert out.returncode != 0
+    assert dt < 30, dt
+    assert f"rank {fail_rank} exited with status" in out.stderr
+    assert "injected failure" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.strip()]  # no result line
