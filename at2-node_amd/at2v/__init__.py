@@ -31,7 +31,7 @@ _POLICIES = {"dalek": POLICY_DALEK_V1, "dalek_v1": POLICY_DALEK_V1, "libsodium":
 # must match include/at2v.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = ("at2v_abi_version", "at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
                     "at2v_verify_one", "at2v_verify_one_policy", "at2v_strerror", "at2v_gen_records_device",
-                    "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
+                    "at2v_gen_records_senders_device", "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
                     "at2v_comm_get_unique_id", "at2v_comm_init_rank", "at2v_verify_shard_gather_device",
                     "at2v_verify_batch_sharded",
                     "at2v_queue_create", "at2v_queue_destroy", "at2v_queue_submit", "at2v_queue_flush",
@@ -68,7 +68,9 @@ SMALL_BATCH_OFF = 0xFFFFFFFF    # include/at2v.h AT2V_SMALL_BATCH_OFF: never use
 class _Info(ctypes.Structure):
     _fields_ = [("num_gpus", ctypes.c_int), ("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
                 ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int), ("vgprs", ctypes.c_int),
-                ("rank", ctypes.c_int), ("world", ctypes.c_int), ("gathers", ctypes.c_uint64)]
+                ("rank", ctypes.c_int), ("world", ctypes.c_int), ("gathers", ctypes.c_uint64),
+                ("cache_entries", ctypes.c_uint64), ("cache_chunks", ctypes.c_uint64),
+                ("cache_chunk_hits", ctypes.c_uint64)]
 
 
 UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)
@@ -123,6 +125,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.at2v_gen_records_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
                                             P, P, P, P, P]
     lib.at2v_gen_records_device.restype = ctypes.c_int
+    lib.at2v_gen_records_senders_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
+                                                    ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P]
+    lib.at2v_gen_records_senders_device.restype = ctypes.c_int
     lib.at2v_sign_batch.argtypes = [P, P, P, P, ctypes.c_size_t, P, P]
     lib.at2v_sign_batch.restype = ctypes.c_int
     lib.at2v_get_info.argtypes = [P, ctypes.POINTER(_Info)]
@@ -260,7 +265,13 @@ class BatchVerifier:
         return unpack_verdicts(words, n)
 
     def gen_records_device(self, cfg_seed: int, first: int, n: int, msg_len: int, d_pk: int, d_sig: int, d_msg: int,
-                           d_off: Optional[int], stream: int = 0) -> None:
+                           d_off: Optional[int], stream: int = 0, senders: int = 0) -> None:
+        """GPU generator; senders > 0: record i is signed by sender (first + i) % senders"""
+        if senders:
+            _check(self._lib.at2v_gen_records_senders_device(self._h, cfg_seed, first, n, msg_len, senders, d_pk, d_sig,
+                                                             d_msg, d_off or None, stream or None),
+                   "at2v_gen_records_senders_device")
+            return
         _check(self._lib.at2v_gen_records_device(self._h, cfg_seed, first, n, msg_len, d_pk, d_sig, d_msg,
                                                  d_off or None, stream or None), "at2v_gen_records_device")
 

@@ -17,22 +17,25 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <random>
 #include <mutex>
 #include <new>
 #include <vector>
 
 #include "../../include/at2v.h"
+#include "at2v_cache.h"
 #include "at2v_shard.h"
 
 namespace at2v {
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream);
+                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache);
 size_t btab_bytes();
 hipError_t launch_build_btab(int4* out, hipStream_t stream);
-hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint8_t* pk, uint8_t* sig,
-                      uint8_t* msg, uint32_t* off, hipStream_t stream);
+hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders, uint8_t* pk,
+                      uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_total, const uint32_t* off, uint32_t n,
                        uint8_t* pk, uint8_t* sig, hipStream_t stream);
 hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStream_t stream);
@@ -64,6 +67,17 @@ struct DevBuf {
   }
 };
 
+// Per-sender A cache of one device (at2v_opts.sender_cache; at2v_cache.h). Launches are serialised by scratch_free, so
+// one set of buffers serves every launch of the context. When a launch finds the cache full, the host learns it from
+// the counters' asynchronous copy and clears the tags before a later launch (eviction = start over).
+struct SenderCache {
+  at2v::CacheArgs args{};
+  DevBuf tags, entries, slot_of, new_list, ctl;
+  unsigned long long* host_ctl = nullptr;  // pinned copy of the device counters, refreshed after every cached launch
+  hipEvent_t ctl_copied = nullptr;
+  bool copy_pending = false;
+};
+
 struct Shard {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -73,6 +87,7 @@ struct Shard {
   int blocks_per_cu = 0;
   int vgprs = 0;
   DevBuf scratch, btab, pk, sig, msg, off, verdict;
+  SenderCache* cache = nullptr;
 };
 
 }  // namespace
@@ -131,6 +146,71 @@ int init_shard(Shard& s, int device) {
 
 bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
+void free_cache(SenderCache*& c) {
+  if (!c) return;
+  c->tags.release();
+  c->entries.release();
+  c->slot_of.release();
+  c->new_list.release();
+  c->ctl.release();
+  if (c->host_ctl) (void)hipHostFree(c->host_ctl);
+  if (c->ctl_copied) (void)hipEventDestroy(c->ctl_copied);
+  delete c;
+  c = nullptr;
+}
+
+// Per-sender cache for `capacity` distinct keys on the current device: 2x as many tag slots (open addressing at
+// load <= 1/2), one entry per slot. AT2V_TEST_CACHE_FP_BITS (tests only) keeps that many fingerprint bits, so distinct
+// keys collide and the byte comparison in the verify kernel is exercised.
+int init_cache(Shard& s, uint32_t capacity, uint64_t seed) {
+  SenderCache* c = new (std::nothrow) SenderCache;
+  if (!c) return AT2V_E_OOM;
+  s.cache = c;
+  uint32_t cap = 1024;
+  while (cap < 2ull * capacity && cap < (1u << 30)) cap <<= 1;
+  c->args.cap = cap;
+  c->args.capacity = capacity < cap / 2 ? capacity : cap / 2;
+  c->args.seed = seed;
+  c->args.fp_mask = ~0ull;
+  if (const char* b = std::getenv("AT2V_TEST_CACHE_FP_BITS")) {
+    const int bits = std::atoi(b);
+    if (bits > 0 && bits < 64) c->args.fp_mask = (1ull << bits) - 1ull;
+  }
+  const size_t ctl_bytes = (size_t)at2v::cache_ctl_words() * 8;
+  AT2V_TRY(c->tags.ensure((size_t)cap * 8));
+  AT2V_TRY(c->entries.ensure((size_t)cap * at2v::cache_entry_bytes()));
+  AT2V_TRY(c->ctl.ensure(ctl_bytes));
+  AT2V_TRY(hipMemset(c->tags.p, 0, c->tags.cap));
+  AT2V_TRY(hipMemset(c->ctl.p, 0, c->ctl.cap));
+  AT2V_TRY(hipHostMalloc((void**)&c->host_ctl, c->ctl.cap, hipHostMallocDefault));
+  std::memset(c->host_ctl, 0, c->ctl.cap);
+  AT2V_TRY(hipEventCreateWithFlags(&c->ctl_copied, hipEventDisableTiming));
+  c->args.tags = (unsigned long long*)c->tags.p;
+  c->args.entries = (int4*)c->entries.p;
+  c->args.ctl = (unsigned long long*)c->ctl.p;
+  return AT2V_OK;
+}
+
+// Before a cached launch: size the per-record slot array, and if an earlier launch found the cache full (its counters'
+// copy has landed), start over: clear the tags and the counters on the stream.
+hipError_t cache_before_launch(SenderCache& c, uint32_t n, hipStream_t stream) {
+  hipError_t e = c.slot_of.ensure((size_t)n * 4);
+  if (e == hipSuccess) e = c.new_list.ensure((size_t)n * 8);
+  if (e != hipSuccess) return e;
+  c.args.slot_of = (int*)c.slot_of.p;
+  c.args.new_list = (uint2*)c.new_list.p;
+  if (c.copy_pending && hipEventQuery(c.ctl_copied) == hipSuccess) {
+    c.copy_pending = false;
+    if (c.host_ctl[at2v::cache_ctl_full()]) {
+      e = hipMemsetAsync(c.tags.p, 0, c.tags.cap, stream);
+      const size_t used = (size_t)at2v::cache_ctl_used(), full = (size_t)at2v::cache_ctl_full();
+      if (e == hipSuccess) e = hipMemsetAsync((unsigned long long*)c.ctl.p + used, 0, 8, stream);
+      if (e == hipSuccess) e = hipMemsetAsync((unsigned long long*)c.ctl.p + full, 0, 8, stream);
+    }
+  }
+  return e;
+}
+
 // One verify launch on shard s (current device = s.device), on `stream`. Launches of a context take turns
 // on the shard's scratch (per-wave tables, chunk-queue counter, pacing lines): this one waits for the
 // previous one, on whatever stream that ran. The verdict words are zeroed first (fail closed).
@@ -139,9 +219,17 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
                         bool zero_verdicts = true) {
   hipError_t e = hipStreamWaitEvent(stream, s.scratch_free, 0);
   if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
+  // the cache serves the throughput kernel (launches above small_batch_max records)
+  SenderCache* c = (s.cache && n > ctx->pair_max) ? s.cache : nullptr;
+  if (e == hipSuccess && c) e = cache_before_launch(*c, n, stream);
   if (e == hipSuccess)
     e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch.p,
-                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream);
+                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &c->args : nullptr);
+  if (e == hipSuccess && c) {
+    e = hipMemcpyAsync(c->host_ctl, c->ctl.p, c->ctl.cap, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipEventRecord(c->ctl_copied, stream);
+    c->copy_pending = e == hipSuccess;
+  }
   if (e == hipSuccess) e = hipEventRecord(s.scratch_free, stream);
   return e;
 }
@@ -198,8 +286,11 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   c->shards.resize((size_t)o.num_gpus);
   int prev = 0;
   (void)hipGetDevice(&prev);
+  std::random_device rd;
   for (int g = 0; g < o.num_gpus; ++g) {
     int rc = init_shard(c->shards[(size_t)g], o.device + g);
+    if (rc == AT2V_OK && o.sender_cache)
+      rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd());
     if (rc != AT2V_OK) {
       (void)hipSetDevice(prev);
       at2v_destroy(c);
@@ -234,6 +325,7 @@ void at2v_destroy(at2v_ctx* ctx) {
   for (Shard& s : ctx->shards) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     if (s.scratch_free) (void)hipEventDestroy(s.scratch_free);
+    free_cache(s.cache);
     s.scratch.release();
     s.btab.release();
     s.pk.release();
@@ -485,6 +577,13 @@ const char* at2v_strerror(int code) {
 
 int at2v_gen_records_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
                             uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg, uint32_t* d_msg_off, void* hip_stream) {
+  return at2v_gen_records_senders_device(ctx, cfg_seed, first, n, msg_len, 0, d_pk, d_sig, d_msg, d_msg_off,
+                                         hip_stream);
+}
+
+int at2v_gen_records_senders_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
+                                    uint64_t senders, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
+                                    uint32_t* d_msg_off, void* hip_stream) {
   if (!ctx) return AT2V_E_INVALID;
   if (n == 0) return AT2V_OK;
   if (!d_pk || !d_sig || (!d_msg && msg_len) || n >= (1u << 31) || (uint64_t)n * msg_len >= (1ull << 32))
@@ -495,7 +594,7 @@ int at2v_gen_records_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, si
   (void)hipGetDevice(&prev);
   hipError_t e = hipSetDevice(s.device);
   if (e == hipSuccess)
-    e = at2v::launch_gen(cfg_seed, first, (uint32_t)n, msg_len, d_pk, d_sig, d_msg, d_msg_off,
+    e = at2v::launch_gen(cfg_seed, first, (uint32_t)n, msg_len, senders, d_pk, d_sig, d_msg, d_msg_off,
                          (hipStream_t)hip_stream);
   (void)hipSetDevice(prev);
   return hip_code(e);
@@ -573,6 +672,20 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
   out->rank = ctx->rank;
   out->world = ctx->comm ? ctx->world : 0;
   out->gathers = ctx->gathers;
+  out->cache_entries = out->cache_chunks = out->cache_chunk_hits = 0;
+  for (const Shard& sh : ctx->shards) {  // sender-cache counters, summed over devices (synchronises the devices)
+    if (!sh.cache) continue;
+    std::vector<unsigned long long> w((size_t)at2v::cache_ctl_words());
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(sh.device) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(w.data(), sh.cache->ctl.p, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      out->cache_entries += w[(size_t)at2v::cache_ctl_used()];
+      out->cache_chunks += w[(size_t)at2v::cache_ctl_chunks()];
+      out->cache_chunk_hits += w[(size_t)at2v::cache_ctl_chunk_hits()];
+    }
+    (void)hipSetDevice(prev);
+  }
   return AT2V_OK;
 }
 

@@ -12,6 +12,7 @@
 //     16-byte loads for A/R/S and 4-byte loads + v_alignbit for unaligned message words.
 #include <hip/hip_runtime.h>
 
+#include "at2v_cache.h"
 #include "at2v_verify.h"
 #include "at2v_verify_fu.h"
 #include "at2v_fe_fu.h"
@@ -288,11 +289,33 @@ struct Pace {
 };
 #endif
 
-// Half-size verification: one chunk of 64 records per wave, no final inversion.
+// ---- per-sender A cache (at2v_opts.sender_cache) ----
+// An entry: key = the 32 bytes of A (2 granules), meta = {dalek decode verdict of A, 0, 0, 0} (1 granule), then the
+// table [j]A, j = 0..8, in DevTabA's per-lane layout (90 granules). Tags: one 64-bit keyed fingerprint per entry (0 =
+// free), open addressing. A fingerprint only nominates an entry: the verify kernel takes it only after comparing all 32
+// key bytes with the record's A, so a collision costs speed, never a verdict.
+constexpr int kCacheEntryGranules = 3 + kTabAGranules;
+enum : int { kCtlUsed = 0, kCtlFull, kCtlNew, kCtlFound, kCtlClaimed, kCtlFailed, kCtlChunkHits, kCtlChunks, kCtlWords };
+
+__device__ AT2V_INLINE bool cache_hit(const int4* __restrict__ cache, int slot, const uint32_t Aw[8], int& ok) {
+  ok = 0;
+  if (slot < 0) return false;
+  const int4* e = cache + (size_t)slot * kCacheEntryGranules;
+  const int4 k0 = e[0], k1 = e[1], m = e[2];
+  ok = m.x;
+  return (uint32_t)k0.x == Aw[0] && (uint32_t)k0.y == Aw[1] && (uint32_t)k0.z == Aw[2] && (uint32_t)k0.w == Aw[3] &&
+         (uint32_t)k1.x == Aw[4] && (uint32_t)k1.y == Aw[5] && (uint32_t)k1.z == Aw[6] && (uint32_t)k1.w == Aw[7];
+}
+
+// Half-size verification: one chunk of 64 records per wave, no final inversion. kCache: the per-sender A
+// cache is on; a wave whose 64 records all hit it skips decoding A and building [j]A (slot_of / cache from
+// cache_lookup_kernel + cache_build_kernel, launched just before on the same stream).
+template <bool kCache>
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
+    const int* __restrict__ slot_of, const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   const int lane = threadIdx.x & 63;
@@ -301,7 +324,15 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t nwords = (n + 31) / 32;
+#ifndef AT2V_EXP_SLOT_WAVES
+#define AT2V_EXP_SLOT_WAVES 0  // EXPERIMENT ONLY (wrong verdicts): > 0 = waves share AT2V_EXP_SLOT_WAVES table slots, so the
+                               // tables' footprint is L2-resident; measures what the table traffic costs in time/clock
+#endif
+#if AT2V_EXP_SLOT_WAVES
+  int4* slot = scratch + ((size_t)(wave % AT2V_EXP_SLOT_WAVES) * 64 + lane) * kLaneGranules;
+#else
   int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
+#endif
   DevTabA ta{slot, astage + wib * 640, lane};
   DevTabA tr{slot + kTabAGranules, rstage + wib * 640, lane};
   const DevTabB tb0{btab, astage + wib * 640, lane};                      // [j]B, staged where A's entry was
@@ -358,7 +389,22 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
       return __builtin_amdgcn_alignbit(hi, lo, sh);
     };
 #if AT2V_FIELD_FU
-    const int good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+    int good;
+    if (kCache) {
+      int a_ok = 0;
+      const bool hit = cache_hit(cache, slot_of[ii], Aw, a_ok);
+      const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
+      DevTabA tc{ta};
+      if (all_hit) tc.base = const_cast<int4*>(cache) + (size_t)slot_of[ii] * kCacheEntryGranules + 3;
+      if (lane == 0) {
+        atomicAdd(cache_ctl + kCtlChunks, 1ull);
+        if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 1ull);
+      }
+      good = verify_half_fu<true>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace, all_hit, a_ok) &
+             (i < n);
+    } else {
+      good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+    }
 #else
     const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
 #endif
@@ -463,10 +509,12 @@ __global__ __launch_bounds__(kPairBlock, 1) void verify_pair_kernel(
   }
 }
 #else
+template <bool kCache>  // the cache applies to the half-size kernel only; here for a common launcher signature
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
+    const int* __restrict__, const int4* __restrict__, unsigned long long* __restrict__) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 bstage[kWavesPerBlock * 8 * 64];
   const int lane = threadIdx.x & 63;
@@ -670,8 +718,9 @@ __device__ AT2V_INLINE void gen_msg_block(uint32_t out16[16], uint64_t cfg, uint
 }
 
 __global__ __launch_bounds__(kBlock) void gen_kernel(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len,
-                                                     uint8_t* __restrict__ pk, uint8_t* __restrict__ sig,
-                                                     uint8_t* __restrict__ msg, uint32_t* __restrict__ off) {
+                                                     uint64_t senders, uint8_t* __restrict__ pk,
+                                                     uint8_t* __restrict__ sig, uint8_t* __restrict__ msg,
+                                                     uint32_t* __restrict__ off) {
   __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
   stage_btab(btab);
   LdsTabB tb{btab};
@@ -679,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(uint64_t cfg, uint64_t firs
   if (i >= n) return;
   const uint64_t idx = first + i;
   uint32_t seed[8];
-  gen_seed(seed, cfg, idx);
+  gen_seed(seed, cfg, senders ? idx % senders : idx);  // key of sender idx % senders; M_i stays per record
   // message bytes into the output buffer (byte stores; msg_len arbitrary)
   uint8_t* m = msg + (size_t)i * msg_len;
   for (uint32_t ctr = 0; ctr * 64 < msg_len; ++ctr) {
@@ -795,6 +844,111 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
   }
 }
 
+// ------------------------------------------------------------------ per-sender A cache kernels
+
+__device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t seed, uint64_t mask) {
+  uint64_t h = seed;
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    h ^= (uint64_t)a[i] | ((uint64_t)a[i + 1] << 32);
+    h *= 0x9e3779b97f4a7c15ull;
+    h ^= h >> 29;
+  }
+  h *= 0xbf58476d1ce4e5b9ull;
+  h ^= h >> 32;
+  return (h & mask) | 1ull;  // never 0 (= free)
+}
+
+// One lane per record: find A's entry by fingerprint (open addressing, 32 probes) or claim a free one (64-bit CAS).
+// slot_of[i] = entry or -1 (no room: the record takes the uncached path). Claimed entries are listed for
+// cache_build_kernel; counters are aggregated per wave (one atomic per wave and counter).
+__global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int slot = -1, claimed = 0, found = 0;
+  if (i < n) {
+    uint32_t a[8];
+    load8(a, pk + (size_t)i * 32);
+    const uint64_t fp = cache_fingerprint(a, c.seed, c.fp_mask);
+    const uint32_t mask = c.cap - 1;
+    const uint32_t h = (uint32_t)(fp >> 17) & mask;
+    for (uint32_t k = 0; k < 32; ++k) {
+      const uint32_t j = (h + k) & mask;
+      const unsigned long long t = __hip_atomic_load(c.tags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == fp) {
+        slot = (int)j;
+        found = 1;
+        break;
+      }
+      if (t != 0) continue;
+      if (__hip_atomic_load(c.ctl + kCtlUsed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c.capacity) break;
+      const unsigned long long old = atomicCAS(c.tags + j, 0ull, (unsigned long long)fp);
+      if (old == 0) {
+        slot = (int)j;
+        claimed = 1;
+        break;
+      }
+      if (old == fp) {
+        slot = (int)j;
+        found = 1;
+        break;
+      }
+    }
+    c.slot_of[i] = slot;
+  }
+  const uint64_t cm = __ballot(claimed), fm = __ballot(found), xm = __ballot(i < n && slot < 0);
+  unsigned long long base = 0;
+  if (lane == 0 && cm) {
+    base = atomicAdd(c.ctl + kCtlNew, (unsigned long long)__popcll(cm));
+    atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(cm));
+    atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
+  }
+  if (lane == 0 && fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
+  if (lane == 0 && xm) {
+    atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
+    atomicExch(c.ctl + kCtlFull, 1ull);
+  }
+  base = __shfl(base, 0);
+  if (claimed) {
+    const uint64_t below = cm & ((1ull << lane) - 1ull);
+    c.new_list[base + (unsigned long long)__popcll(below)] = make_uint2((uint32_t)slot, i);
+  }
+}
+
+// One lane per entry claimed by this launch: key, dalek decode verdict and [j]A (build_a_table, the verify kernel's own
+// steps). Threads beyond the launch's claim count leave at once.
+__global__ __launch_bounds__(256) void cache_build_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if ((unsigned long long)t >= __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const uint2 e = c.new_list[t];
+  uint32_t a[8];
+  load8(a, pk + (size_t)e.y * 32);
+  int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
+  DevTabA tw{ent + 3, nullptr, 0};
+  const int ok = build_a_table(a, tw);
+  ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
+  ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
+  ent[2] = make_int4(ok, 0, 0, 0);
+}
+
+size_t cache_entry_bytes() { return (size_t)kCacheEntryGranules * 16; }
+int cache_ctl_words() { return kCtlWords; }
+int cache_ctl_used() { return kCtlUsed; }
+int cache_ctl_full() { return kCtlFull; }
+int cache_ctl_chunk_hits() { return kCtlChunkHits; }
+int cache_ctl_chunks() { return kCtlChunks; }
+
+hipError_t launch_cache_prepare(const CacheArgs& c, const uint8_t* pk, uint32_t n, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(c.ctl + kCtlNew, 0, sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(cache_lookup_kernel, dim3(blocks), dim3(256), 0, stream, pk, n, c);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cache_build_kernel, dim3(blocks), dim3(256), 0, stream, pk, c);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launchers (host side)
 
 size_t btab_bytes() { return (size_t)kNumBtabs * kBtabEntries * 8 * 16; }
@@ -812,7 +966,7 @@ hipError_t launch_build_btab(int4* out, hipStream_t stream) {
 
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream) {
+                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache) {
   if (n == 0) return hipSuccess;
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
   if (n <= pair_max) {
@@ -833,16 +987,25 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesPerBlock);
   const hipError_t me = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
   if (me != hipSuccess) return me;
-  hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                     verdicts, scratch, btab, queue);
+#if AT2V_VERIFY_HALF && AT2V_FIELD_FU
+  if (cache) {
+    const hipError_t ce = launch_cache_prepare(*cache, pk, n, stream);
+    if (ce != hipSuccess) return ce;
+    hipLaunchKernelGGL(verify_kernel<true>, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+                       verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL(verify_kernel<false>, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+                     verdicts, scratch, btab, queue, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
-hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint8_t* pk, uint8_t* sig,
-                      uint8_t* msg, uint32_t* off, hipStream_t stream) {
+hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders, uint8_t* pk,
+                      uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(gen_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, cfg, first, n, msg_len, pk,
-                     sig, msg, off);
+  hipLaunchKernelGGL(gen_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, cfg, first, n, msg_len,
+                     senders, pk, sig, msg, off);
   return hipGetLastError();
 }
 
@@ -861,10 +1024,10 @@ hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStrea
 }
 
 hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs) {
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, verify_kernel, kBlock, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, verify_kernel<false>, kBlock, 0);
   if (e != hipSuccess) return e;
   hipFuncAttributes attr;
-  e = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(verify_kernel));
+  e = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(verify_kernel<false>));
   if (e == hipSuccess && vgprs) *vgprs = attr.numRegs;
   return e;
 }

@@ -14,10 +14,16 @@
 
 namespace at2v {
 
-template <class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax, class Pace = NoPace>
+// kCacheable: the per-sender A cache is on (at2v_opts.sender_cache). Then a_cached = 1 (wave-uniform: every lane of the
+// wave found its A in the cache, confirmed byte for byte) means `ta` already holds the lane's [j]A table (the cache
+// entry) and a_cached_ok is dalek's decode verdict for A; only R is decoded and only R's table is built. Everything the
+// verdict depends on is still a function of (A, R||S, M) alone.
+template <bool kCacheable = false, class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax,
+          class Pace = NoPace>
 AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                        MsgWord msgword, int policy, TabP& ta, TabP& tr, const TabB0& tb0,
-                                       const TabB1& tb1, WaveMax wave_max, Pace&& pace = Pace()) {
+                                       const TabB1& tb1, WaveMax wave_max, Pace&& pace = Pace(), int a_cached = 0,
+                                       int a_cached_ok = 0) {
   // V1: s < l
   int ok = sc_is_canonical(Sw);
   if (policy == POLICY_LIBSODIUM_1_0_18) {
@@ -26,7 +32,9 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   }
   // V2: decode A and R together; R must be canonical (y < p, not x = 0 with the sign bit)
   gu_p3 A, R;
-  {
+  if (kCacheable && a_cached) {
+    ok &= gu_frombytes(R, Rw) & a_cached_ok;
+  } else {
     int okd[2];
     gu_frombytes_x2(A, Aw, R, Rw, okd);
     ok &= okd[0] & okd[1];
@@ -78,7 +86,22 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     fu_neg(R.T, R.T, FU_KC);
     fu_carry(R.T);
   }
-  {
+  if (kCacheable && a_cached) {  // [j]A comes from the cache entry: build [j](+-R) alone
+    gu_cached cr1, cj;
+    gu_cached_identity(cj);
+    tr.store(0, cj);
+    gu_p3_to_cached(cr1, R);
+    tr.store(1, cr1);
+    gu_p3 PR = R;
+#pragma unroll 1
+    for (int j = 2; j <= 8; ++j) {
+      gu_p1p1 sr;
+      gu_add(sr, PR, cr1);
+      gu_p1p1_to_p3(PR, sr);
+      gu_p3_to_cached(cj, PR);
+      tr.store(j, cj);
+    }
+  } else {
     gu_cached ca1, cr1, cj;
     gu_cached_identity(cj);
     ta.store(0, cj);
@@ -339,6 +362,34 @@ AT2V_HD AT2V_INLINE int verify_pair_combine(const gu_p3& mine, const gu_cached& 
   fu d;
   fu_sub(d, v.T, v.Y, FU_K2C);  // F + K - H: H = B + A is a sum of two carried elements, F may exceed FU_KC
   return fu_iszero(v.X) & fu_iszero(d);
+}
+
+}  // namespace at2v
+
+namespace at2v {
+
+// Per-sender cache entry (at2v_opts.sender_cache; AT2 senders repeat, accounts/account.rs:36-43): dalek's decode verdict
+// for A and the table [j]A, j = 0..8, built by exactly the steps verify_half_fu uses for its own [j]A, in the layout it
+// reads through `ta`. Returns the decode verdict (the table is unused when it is 0).
+template <class TabP>
+AT2V_HD AT2V_INLINE int build_a_table(const uint32_t Aw[8], TabP& ta) {
+  gu_p3 A;
+  const int ok = gu_frombytes(A, Aw);
+  gu_cached ca1, cj;
+  gu_cached_identity(cj);
+  ta.store(0, cj);
+  gu_p3_to_cached(ca1, A);
+  ta.store(1, ca1);
+  gu_p3 PA = A;
+#pragma unroll 1
+  for (int j = 2; j <= 8; ++j) {
+    gu_p1p1 sa;
+    gu_add(sa, PA, ca1);
+    gu_p1p1_to_p3(PA, sa);
+    gu_p3_to_cached(cj, PA);
+    ta.store(j, cj);
+  }
+  return ok;
 }
 
 }  // namespace at2v

@@ -95,6 +95,9 @@ pub struct At2vInfo {
     pub rank: c_int,
     pub world: c_int,
     pub gathers: u64,
+    pub cache_entries: u64,
+    pub cache_chunks: u64,
+    pub cache_chunk_hits: u64,
 }
 
 /// `Default`: device 0, DALEK_V1, and the library defaults for every size (65536 records, 1 ms, 256 B, depth 3).
@@ -178,6 +181,9 @@ extern "C" {
     pub fn at2v_gen_records_device(ctx: *mut At2vCtx, cfg_seed: u64, first: u64, n: usize, msg_len: u32,
                                    d_pk: *mut u8, d_sig: *mut u8, d_msg: *mut u8, d_msg_off: *mut u32,
                                    hip_stream: *mut c_void) -> c_int;
+    pub fn at2v_gen_records_senders_device(ctx: *mut At2vCtx, cfg_seed: u64, first: u64, n: usize, msg_len: u32,
+                                           senders: u64, d_pk: *mut u8, d_sig: *mut u8, d_msg: *mut u8,
+                                           d_msg_off: *mut u32, hip_stream: *mut c_void) -> c_int;
     pub fn at2v_sign_batch(ctx: *mut At2vCtx, seeds: *const u8, msg: *const u8, msg_off: *const u32, n: usize,
                            pk_out: *mut u8, sig_out: *mut u8) -> c_int;
     pub fn at2v_get_info(ctx: *mut At2vCtx, out: *mut At2vInfo) -> c_int;

@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--records-per-gpu", type=int, default=1 << 20)
     ap.add_argument("--msg-len", type=int, default=100)
     ap.add_argument("--policy", default="dalek")
+    ap.add_argument("--senders", type=int, default=0,
+                    help="0 = distinct keys (BASELINE config 2); K > 0 = record i signed by sender i %% K (AT2 traffic)")
+    ap.add_argument("--sender-cache", type=int, default=0,
+                    help="at2v_opts.sender_cache: per-sender A cache capacity in keys (0 = off)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="max records for the CPU baseline sample (0 = skip); sized to ~3 s on the threads used")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
@@ -185,7 +189,7 @@ def main():
 
     n, L = args.records_per_gpu, args.msg_len
     n = (n + 63) // 64 * 64
-    v = at2v.BatchVerifier(device=local, policy=args.policy)
+    v = at2v.BatchVerifier(device=local, policy=args.policy, sender_cache=args.sender_cache)
     if use_dist:
         uid = [at2v.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -201,7 +205,7 @@ def main():
     d_all = torch.zeros(words * world, dtype=torch.int32, device=dev)  # node bitmap (N > 1)
     # distinct records per rank (indices rank*n .. rank*n+n-1)
     v.gen_records_device(CFG_SEED, rank * n, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
-                         d_off.data_ptr(), s)
+                         d_off.data_ptr(), s, senders=args.senders)
     torch.cuda.synchronize(dev)
 
     def verify(pk, sig, msg, off, strm):
@@ -257,6 +261,9 @@ def main():
     if rank == 0:
         if world == 8 and n == 2 * (1 << 20):
             workload = "BASELINE config 3: 16M signatures index-sharded over 8 MI355X + RCCL all-gather of the verdict bitmap"
+        elif args.senders:
+            workload = (f"{n} signed transfers per GPU ({L}-byte M) from {args.senders} repeating senders (AT2 traffic)"
+                        + (f", per-sender A cache of {args.sender_cache} keys" if args.sender_cache else ", no cache"))
         elif n == 1 << 20:
             workload = (f"BASELINE config 2: 1M signed transfers per GPU (100-byte M), dalek-1.x verify"
                         + (f"; {world} GPUs, weak scaling, RCCL all-gather of the verdict bitmap" if world > 1 else ""))
@@ -280,6 +287,8 @@ def main():
                 "records_per_gpu": n,
                 "msg_len": L,
                 "policy": args.policy,
+                "senders": args.senders or "distinct",
+                "sender_cache": args.sender_cache,
                 "parallelism": f"index-shard x{world}" + (" + RCCL all-gather of verdict words (libat2v)" if use_dist else ""),
             },
             "verdict_match": match,
@@ -435,7 +444,7 @@ def _pmc_pass(args, n, L, counters):
     cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", *counters, "--kernel-trace", "--output-format", "csv",
            "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "0",
            "--cpu-sample", "0", "--pmc-traffic", "0", "--records-per-gpu", str(n), "--msg-len", str(L),
-           "--policy", args.policy]
+           "--policy", args.policy, "--senders", str(args.senders), "--sender-cache", str(args.sender_cache), "--e2e", "0"]
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150, check=True)
         rows, durs = [], []

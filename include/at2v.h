@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
- * version 3 appended at2v_opts.sender_cache and at2v_info.gathers and the AT2V_E_PEER code (version 2 appended
+ * version 3 appended at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
  * at2v_opts.small_batch_max and at2v_queue_opts.flags). A binding checks at2v_abi_version() == AT2V_ABI_VERSION
  * before passing any struct (the Python and Rust bindings in this repo refuse a mismatching library). */
 #define AT2V_ABI_VERSION 3
@@ -120,6 +120,12 @@ const char* at2v_strerror(int code);
 int at2v_gen_records_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
                             uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg, uint32_t* d_msg_off, void* hip_stream);
 
+/* The same with repeating senders (AT2 traffic: accounts/account.rs:36-43): record i is signed by the key of seed index
+ * (first + i) % senders, its message is still M_i. senders = 0: distinct keys (= at2v_gen_records_device). */
+int at2v_gen_records_senders_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
+                                    uint64_t senders, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
+                                    uint32_t* d_msg_off, void* hip_stream);
+
 /* RFC 8032 signing of host messages under 32-byte seeds (host buffers, synchronous). pk_out n x 32,
  * sig_out n x 64. The GPU counterpart of KeyPair::sign (drop), used by tests and the bench generator. */
 int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, const uint32_t* msg_off, size_t n,
@@ -136,6 +142,9 @@ typedef struct {
   int rank;            /* at2v_comm_init_rank: this context's rank, else 0 */
   int world;           /* at2v_comm_init_rank: ranks in the communicator, else 0 */
   uint64_t gathers;    /* verdict all-gathers this context has issued (failure paths included) */
+  uint64_t cache_entries;    /* at2v_opts.sender_cache: distinct senders now cached (all devices) */
+  uint64_t cache_chunks;     /* 64-record chunks verified with the cache on */
+  uint64_t cache_chunk_hits; /* ... of which every record's A came from the cache (A decode and [j]A skipped) */
 } at2v_info;
 int at2v_get_info(at2v_ctx* ctx, at2v_info* out);
 

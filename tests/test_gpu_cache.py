@@ -1,0 +1,150 @@
+"""GPU: the per-sender A cache (at2v_opts.sender_cache; VERDICT r2 item 6, SURVEY §7 "reusing per-sender A tables").
+
+AT2 senders issue consecutive sequences (/root/reference/src/bin/server/accounts/account.rs:36-43), so one key signs many
+payloads of a node batch (client.rs:77-78). With the cache on, a wave whose 64 records all find their A in the cache
+(fingerprint nominates an entry, then all 32 key bytes are compared) skips decoding A and building [j]A. The verdict
+must stay a pure function of (A, R||S, M): every test here compares with the oracle or the golden fixtures, through
+the C ABI, in every cache state — entry built in the same launch, warm, fingerprint collisions (forced with
+AT2V_TEST_CACHE_FP_BITS), cache full (restart), undecodable / small-order / non-canonical senders cached together with
+their decode verdict, and both policies."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io
+
+pytestmark = pytest.mark.gpu
+
+CFG_SEED = 0x4154325F
+OFF = 0xFFFFFFFF  # small_batch_max: the cache serves the throughput kernel, so run it at every size
+
+
+@pytest.fixture(scope="module")
+def at2v_mod():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import at2v
+    return at2v
+
+
+def _mutate(pk, sig, msg, off, rng, k):
+    """k records mutated in R, S, M or A (a bit flip): each then has exactly one verdict the oracle decides"""
+    pk, sig, msg = pk.copy(), sig.copy(), msg.copy()
+    for i in rng.choice(len(pk), k, replace=False):
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            sig[i, rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
+        elif kind == 1:
+            sig[i, 32 + rng.integers(0, 31)] ^= 1 << rng.integers(0, 8)
+        elif kind == 2 and off[i + 1] > off[i]:
+            msg[off[i] + rng.integers(0, off[i + 1] - off[i])] ^= 1
+        else:
+            pk[i, rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
+    return pk, sig, msg
+
+
+def test_config1_traffic_every_chunk_hits(at2v_mod, oracle):
+    """BASELINE config 1 traffic (64 senders x sequences 1..64): every entry is built by the first launch's build pass,
+    so every chunk of every launch takes the cached path; verdicts equal the oracle's, mutated records included."""
+    pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
+    rng = np.random.default_rng(3)
+    pk2, sig2, msg2 = _mutate(pk, sig, msg, off, rng, 300)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    want2 = oracle.verify_batch(pk2, sig2, msg2, off)
+    assert want.all() and 0 < want2.sum() < len(want2)
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024) as v:
+        for rep in range(2):
+            assert np.array_equal(v.verify_batch(pk, sig, msg, off), want)
+        info = v.info()
+        assert info["cache_entries"] == 64
+        assert info["cache_chunks"] == 2 * 64 and info["cache_chunk_hits"] == info["cache_chunks"]
+        got2 = v.verify_batch(pk2, sig2, msg2, off)  # mutated A's are new keys: new entries, some undecodable
+        assert np.array_equal(got2, want2), np.nonzero(got2 != want2)[0][:10]
+        assert v.info()["cache_entries"] > 64
+
+
+@pytest.mark.parametrize("policy", ["dalek", "libsodium"])
+def test_golden_sets_with_cache(at2v_mod, golden, policy):
+    """every golden fixture set, twice (cold, then warm cache), both policies: the small-order, non-canonical and
+    off-curve senders of the adversarial/edge sets are cached with their decode verdicts"""
+    with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 15) as v:
+        for name in golden_io.SETS:
+            g = golden[name]
+            want = g.dalek if policy == "dalek" else g.sodium
+            for rep in range(2):
+                got = v.verify_batch(g.pk, g.sig, g.msg, g.off)
+                assert np.array_equal(got, want), (name, rep, np.nonzero(got != want)[0][:10])
+
+
+def test_repeated_adversarial_senders(at2v_mod, oracle):
+    """an adversarial batch whose senders repeat: 512 distinct records (every class of config 4) tiled 32x with fresh
+    mutations, so entries for small-order / undecodable keys are hit by many records"""
+    pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 21, 0, 512, 100)
+    L = 100
+    pk_t = np.tile(pk, (32, 1))
+    sig_t = np.tile(sig, (32, 1))
+    msg_t = np.tile(msg, 32)
+    off_t = (np.arange(512 * 32 + 1) * L).astype(np.uint32)
+    pk_t, sig_t, msg_t = _mutate(pk_t, sig_t, msg_t, off_t, np.random.default_rng(5), 1500)
+    want = oracle.verify_batch(pk_t, sig_t, msg_t, off_t)
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=4096) as v:
+        for rep in range(2):
+            got = v.verify_batch(pk_t, sig_t, msg_t, off_t)
+            assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+def test_fingerprint_collisions_fall_back(at2v_mod, oracle, monkeypatch):
+    """3 fingerprint bits (test hook): distinct senders share fingerprints, so the lookup nominates entries of other
+    keys; the byte comparison must send those waves down the uncached path with identical verdicts"""
+    monkeypatch.setenv("AT2V_TEST_CACHE_FP_BITS", "3")
+    pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
+    pk2, sig2, msg2 = _mutate(pk, sig, msg, off, np.random.default_rng(7), 200)
+    want = oracle.verify_batch(pk2, sig2, msg2, off)
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024) as v:
+        for rep in range(2):
+            assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want)
+        info = v.info()
+        assert info["cache_entries"] <= 4 and info["cache_chunk_hits"] < info["cache_chunks"]
+
+
+def test_cache_full_restarts(at2v_mod, oracle):
+    """capacity 16 < 64 senders: the first launch fills the cache (the rest go uncached), a later launch starts over;
+    verdicts exact throughout"""
+    pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
+    pk2, sig2, msg2 = _mutate(pk, sig, msg, off, np.random.default_rng(9), 100)
+    want = oracle.verify_batch(pk2, sig2, msg2, off)
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=16) as v:
+        for rep in range(4):
+            assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want), rep
+            assert v.info()["cache_entries"] <= 16
+
+
+def test_generator_with_repeating_senders(at2v_mod, oracle):
+    """at2v_gen_records_senders_device: record i signed by sender i % senders, M_i per record, all valid (oracle)"""
+    import torch
+    n, L, S = 4096, 100, 64
+    dev = "cuda:0"
+    d_pk = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    d_sig = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+    d_msg = torch.zeros(n * L, dtype=torch.uint8, device=dev)
+    d_off = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    with at2v_mod.BatchVerifier() as v:
+        v.gen_records_device(CFG_SEED, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream, senders=S)
+        torch.cuda.synchronize()
+    pk = d_pk.cpu().numpy().reshape(n, 32)
+    sig = d_sig.cpu().numpy().reshape(n, 64)
+    msg = d_msg.cpu().numpy()
+    off = d_off.cpu().numpy().astype(np.uint32)
+    assert (pk == np.tile(pk[:S], (n // S, 1))).all() and len({bytes(r) for r in pk[:S]}) == S
+    assert oracle.verify_batch(pk, sig, msg, off).all()
+    # the sender keys are the distinct-key generator's keys 0..S-1
+    with at2v_mod.BatchVerifier() as v:
+        d2 = torch.zeros(S * 32, dtype=torch.uint8, device=dev)
+        ds = torch.zeros(S * 64, dtype=torch.uint8, device=dev)
+        dm = torch.zeros(S * L, dtype=torch.uint8, device=dev)
+        v.gen_records_device(CFG_SEED, 0, S, L, d2.data_ptr(), ds.data_ptr(), dm.data_ptr(), None,
+                             torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    assert (d2.cpu().numpy().reshape(S, 32) == pk[:S]).all()

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--msg-len", type=int, default=100)
+    ap.add_argument("--no-check", action="store_true", help="perf-only experiment builds: skip the verdict check")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L = a.n, a.msg_len
@@ -59,7 +60,7 @@ def main():
             ok = bool((d_ver == -1).all().item())
             if r > 0:
                 times[p].append(e0.elapsed_time(e1))
-            assert ok, f"{p}: wrong verdicts"
+            assert ok or a.no_check, f"{p}: wrong verdicts"
     for p in a.libs:
         t = np.array(times[p])
         print(f"{os.path.basename(p):28s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  -> {n / np.median(t) / 1e3:8.2f} M verifies/s")
