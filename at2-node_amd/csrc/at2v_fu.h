@@ -143,13 +143,38 @@ AT2V_HD AT2V_INLINE int fu_isnegative(const fu& f) {
 
 // ------------------------------------------------------------------ exponentiation (carried inputs)
 
-AT2V_HD AT2V_INLINE void fu_sqn(fu& h, const fu& f, int n) {  // h = f^(2^n), n >= 1, loop kept rolled
+// Squaring chains, loops kept rolled. AT2V_SQN_PINGPONG: the loop body squares twice, into a second register set and
+// back, so no iteration ends with copying the square over its input (the in-place form costs ~10 v_mov per square).
+#ifndef AT2V_SQN_PINGPONG
+#define AT2V_SQN_PINGPONG 1
+#endif
+AT2V_HD AT2V_INLINE void fu_sqn(fu& h, const fu& f, int n) {  // h = f^(2^n), n >= 1
   fu_sqc(h, f);
+#if AT2V_SQN_PINGPONG
+  int i = 1;
+  for (; i + 1 < n; i += 2) {
+    fu t;
+    fu_sqc(t, h);
+    fu_sqc(h, t);
+  }
+  if (i < n) fu_sqc(h, h);
+#else
   for (int i = 1; i < n; ++i) fu_sqc(h, h);
+#endif
 }
 AT2V_HD AT2V_INLINE void fu_sqn_x2(fu& h0, const fu& f0, fu& h1, const fu& f1, int n) {
   fu_sqc_x2(h0, f0, h1, f1);
+#if AT2V_SQN_PINGPONG
+  int i = 1;
+  for (; i + 1 < n; i += 2) {
+    fu t0, t1;
+    fu_sqc_x2(t0, h0, t1, h1);
+    fu_sqc_x2(h0, t0, h1, t1);
+  }
+  if (i < n) fu_sqc_x2(h0, h0, h1, h1);
+#else
   for (int i = 1; i < n; ++i) fu_sqc_x2(h0, h0, h1, h1);
+#endif
 }
 
 // z250 = z^(2^250 - 1), z11 = z^11 (shared prefix of invert and pow22523)

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""latency_probe.py — where a small batch's latency goes (BASELINE config 5).
+
+For batches of B records (default 1, 20, 64, 1024), each measured `--reps` times on one MI355X:
+  kernel   : HIP events around at2v_verify_batch_device on HBM-resident records (the low-latency kernel for
+             B <= small_batch_max), i.e. device time of the launch;
+  sync     : wall time of at2v_verify_batch (host arrays: H2D, kernel, D2H, synchronise);
+  queue    : wall time from at2v_queue_submit of the B records to the last verdict polled (eager queue, idle,
+             one batch in flight at a time);
+reports p50/p90 per stage as JSON. Records come from the oracle generator (all valid), checked once per size."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def pct(xs, q):
+    return float(np.percentile(np.asarray(xs), q))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1,20,64,1024")
+    ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--msg-len", type=int, default=48)
+    a = ap.parse_args()
+    import torch
+
+    import at2v
+    import oracle_py
+    from at2v.node import IngestQueue
+
+    torch.cuda.set_device(0)
+    o = oracle_py.Oracle()
+    sizes = [int(x) for x in a.sizes.split(",")]
+    nmax = max(sizes)
+    pk, sig, msg, off = o.gen_records(0x4154325F, 0, nmax, a.msg_len)
+    out = {"msg_len": a.msg_len, "reps": a.reps, "sizes": {}}
+    v = at2v.BatchVerifier(device=0)
+    q = IngestQueue(device=0, max_batch=4096, max_delay_us=1000, eager=True)
+    s = torch.cuda.current_stream()
+    for B in sizes:
+        p, g, m, f = pk[:B], sig[:B], msg[:f_end(off, B)], off[:B + 1]
+        assert v.verify_batch(p, g, m, f).all()
+        d_pk = torch.from_numpy(p.reshape(-1).copy()).cuda()
+        d_sig = torch.from_numpy(g.reshape(-1).copy()).cuda()
+        d_msg = torch.from_numpy(np.concatenate([m, np.zeros(16, np.uint8)])).cuda()
+        d_off = torch.from_numpy(f.view(np.int32).copy()).cuda()
+        d_ver = torch.zeros((B + 31) // 32, dtype=torch.int32, device="cuda")
+        kern, sync, queue = [], [], []
+        for r in range(a.reps + 5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            v.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), int(f[-1]), d_off.data_ptr(), B,
+                                  d_ver.data_ptr(), s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            v.verify_batch(p, g, m, f)
+            t1 = time.perf_counter()
+            first = q.submit(p, g, m, f)
+            got = 0
+            while got < B:
+                t, vv = q.poll(4096, 2000)
+                got += len(t)
+            t2 = time.perf_counter()
+            if r >= 5:
+                kern.append(e0.elapsed_time(e1) * 1e3)
+                sync.append((t1 - t0) * 1e6)
+                queue.append((t2 - t1) * 1e6)
+        assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
+        out["sizes"][B] = {k: {"p50_us": pct(x, 50), "p90_us": pct(x, 90)} for k, x in
+                           (("kernel", kern), ("sync", sync), ("queue", queue))}
+        print(B, json.dumps(out["sizes"][B]), file=sys.stderr)
+    q.close()
+    v.close()
+    print(json.dumps(out))
+
+
+def f_end(off, B):
+    return int(off[B])
+
+
+if __name__ == "__main__":
+    main()
