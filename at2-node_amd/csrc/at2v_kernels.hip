@@ -103,6 +103,29 @@ struct DevTabA {
 #pragma unroll
     for (int q = 0; q < 10; ++q) base[e * 10 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
+  // a decoded point parked in entry 8's space (verify_half_fu, AT2V_PARK_POINTS): 10 stores now, 10 loads and one wait
+  // at unpark; entry 8 is the last one the table build writes
+  template <class P3>
+  __device__ AT2V_INLINE void park(const P3& p) const {
+    static_assert(sizeof(P3) == 160, "p3 point: 40 words");
+    const int32_t* w = reinterpret_cast<const int32_t*>(&p);
+#pragma unroll
+    for (int q = 0; q < 10; ++q) base[80 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+  template <class P3>
+  __device__ AT2V_INLINE void unpark(P3& p) const {
+    int32_t* w = reinterpret_cast<int32_t*>(&p);
+    int4 v[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) v[q] = base[80 + q];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      w[4 * q] = v[q].x;
+      w[4 * q + 1] = v[q].y;
+      w[4 * q + 2] = v[q].z;
+      w[4 * q + 3] = v[q].w;
+    }
+  }
   __device__ AT2V_INLINE void load(int e, ge_cached& c) const {
     int32_t* w = reinterpret_cast<int32_t*>(&c);
 #pragma unroll

@@ -18,6 +18,10 @@ namespace at2v {
 // wave found its A in the cache, confirmed byte for byte) means `ta` already holds the lane's [j]A table (the cache
 // entry) and a_cached_ok is dalek's decode verdict for A; only R is decoded and only R's table is built. Everything the
 // verdict depends on is still a function of (A, R||S, M) alone.
+#ifndef AT2V_PARK_POINTS
+#define AT2V_PARK_POINTS 1  // decoded A and R parked in the table slots across SHA-512 / lattice (0: kept live)
+#endif
+
 template <bool kCacheable = false, class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax,
           class Pace = NoPace>
 AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
@@ -41,6 +45,14 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   }
   ok &= enc_y_canonical(Rw);
   ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
+#if AT2V_PARK_POINTS
+  // A and R are not used again until the tables are built (after SHA-512, the lattice reduction and the recoding), and
+  // holding their 80 words through those phases is what makes the compiler spill (one scratch reload and wait per
+  // word, ~50 of them at the table build). Park them in the lanes' table slots (entry 8, written last by the build)
+  // with 20 fire-and-forget stores; reload them with 20 loads and one wait where the build starts.
+  if (!(kCacheable && a_cached)) ta.park(A);
+  tr.park(R);
+#endif
   AT2V_PHASE(1);
   pace.mark(10);
   // V3: k = SHA-512(R || A || M) mod l
@@ -80,6 +92,10 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   pace.mark(1);
 
   // tables [j]A and [j](+-R), j = 0..8, built as one interleaved pair
+#if AT2V_PARK_POINTS
+  if (!(kCacheable && a_cached)) ta.unpark(A);
+  tr.unpark(R);
+#endif
   if (hs.c1_neg) {
     fu_neg(R.X, R.X, FU_KC);
     fu_carry(R.X);

@@ -83,6 +83,9 @@ struct HostTabAFu {
   gu_cached e[9];
   int pending = 0;
   void store(int i, const gu_cached& c) { e[i] = c; }
+  gu_p3 parked;
+  void park(const gu_p3& p) { parked = p; }
+  void unpark(gu_p3& p) const { p = parked; }
   void prefetch(int i) { pending = i; }
   void load_prefetched(gu_cached& c) const { c = e[pending]; }
 };

@@ -7,8 +7,10 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $D/gpu_tests.txt 2>&1 || { tail -40 $D/gpu_tests.txt; exit 1; }
 tail -3 $D/gpu_tests.txt
 V=at2-node_amd/at2v/variants
-timeout -k 10 300 python3 tools/ab_bench.py $V/libat2v_base.so $V/libat2v_cur.so $V/libat2v_nopp.so $V/libat2v_slot8.so $V/libat2v_slot256.so --rounds 8 --no-check > $D/ab_slots.txt 2>&1 || { tail -20 $D/ab_slots.txt; exit 1; }
+timeout -k 10 300 python3 tools/ab_bench.py $V/libat2v_base.so $V/libat2v_nopp.so $V/libat2v_pp.so $V/libat2v_park.so $V/libat2v_slot8.so $V/libat2v_slot256.so --rounds 8 --no-check > $D/ab_slots.txt 2>&1 || { tail -20 $D/ab_slots.txt; exit 1; }
 cat $D/ab_slots.txt
+timeout -k 10 300 python3 tools/latency_probe.py --reps 100 > $D/latency_probe.json 2> $D/latency_probe.err || { tail -20 $D/latency_probe.err; exit 1; }
+cat $D/latency_probe.err
 timeout -k 10 300 python3 bench.py --senders 64 --sender-cache 0 --cpu-sample 0 --pmc-traffic 0 --e2e 0 --steps 10 > $D/bench_s64_nocache.json 2> $D/b1.err || { tail -20 $D/b1.err; exit 1; }
 timeout -k 10 300 python3 bench.py --senders 64 --sender-cache 4096 --cpu-sample 0 --pmc-traffic 0 --e2e 0 --steps 10 > $D/bench_s64_cache.json 2> $D/b2.err || { tail -20 $D/b2.err; exit 1; }
 python3 -c "
