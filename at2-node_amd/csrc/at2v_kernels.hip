@@ -883,28 +883,45 @@ __device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t 
 }
 
 // One lane per record: find A's entry by fingerprint (open addressing, 32 probes) or claim a free one (64-bit CAS).
-// slot_of[i] = entry or -1 (no room: the record takes the uncached path). Claimed entries are listed for
-// cache_build_kernel; counters are aggregated per wave (one atomic per wave and counter).
+// slot_of[i] = entry or -1 (no room: the record takes the uncached path). Claims are reserved against the capacity per
+// wave (one atomic on the `used` counter for the wave's claimants, unused reservations given back), so the capacity
+// holds to within what concurrent waves have reserved but not yet returned. Claimed entries are listed for
+// cache_build_kernel; the statistics counters are aggregated per wave.
 __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  int slot = -1, claimed = 0, found = 0;
+  const uint32_t mask = c.cap - 1;
+  int slot = -1, claimed = 0, found = 0, want = 0;
+  uint64_t fp = 0;
+  uint32_t h = 0, k = 0;
   if (i < n) {
     uint32_t a[8];
     load8(a, pk + (size_t)i * 32);
-    const uint64_t fp = cache_fingerprint(a, c.seed, c.fp_mask);
-    const uint32_t mask = c.cap - 1;
-    const uint32_t h = (uint32_t)(fp >> 17) & mask;
-    for (uint32_t k = 0; k < 32; ++k) {
-      const uint32_t j = (h + k) & mask;
-      const unsigned long long t = __hip_atomic_load(c.tags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fp = cache_fingerprint(a, c.seed, c.fp_mask);
+    h = (uint32_t)(fp >> 17) & mask;
+    for (; k < 32; ++k) {  // phase 1: find the key, or the first free slot on its probe path
+      const unsigned long long t = __hip_atomic_load(c.tags + ((h + k) & mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == fp) {
-        slot = (int)j;
+        slot = (int)((h + k) & mask);
         found = 1;
         break;
       }
-      if (t != 0) continue;
-      if (__hip_atomic_load(c.ctl + kCtlUsed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c.capacity) break;
+      if (t == 0) {
+        want = 1;
+        break;
+      }
+    }
+  }
+  // reserve the wave's claims against the capacity
+  const uint64_t wm = __ballot(want);
+  unsigned long long base = 0;
+  if (lane == 0 && wm) base = atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(wm));
+  base = __shfl(base, 0);
+  const unsigned long long my = base + (unsigned long long)__popcll(wm & ((1ull << lane) - 1ull));
+  const int denied = want && my >= c.capacity;
+  if (want && !denied) {  // phase 2: claim along the probe path (a racing claimant may take the slot first)
+    for (; k < 32; ++k) {
+      const uint32_t j = (h + k) & mask;
       const unsigned long long old = atomicCAS(c.tags + j, 0ull, (unsigned long long)fp);
       if (old == 0) {
         slot = (int)j;
@@ -917,25 +934,37 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
         break;
       }
     }
-    c.slot_of[i] = slot;
   }
+  if (denied) {  // phase 3: a lane of this wave with the same key may have claimed it meanwhile (same probe path)
+    for (uint32_t q = 0; q < 32; ++q) {
+      const uint32_t j = (h + q) & mask;
+      const unsigned long long t = __hip_atomic_load(c.tags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == fp) {
+        slot = (int)j;
+        found = 1;
+        break;
+      }
+      if (t == 0) break;
+    }
+  }
+  if (i < n) c.slot_of[i] = slot;
   const uint64_t cm = __ballot(claimed), fm = __ballot(found), xm = __ballot(i < n && slot < 0);
-  unsigned long long base = 0;
-  if (lane == 0 && cm) {
-    base = atomicAdd(c.ctl + kCtlNew, (unsigned long long)__popcll(cm));
-    atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(cm));
-    atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
+  const uint64_t unused = wm & ~cm;  // reservations not turned into claims (denied, found, or no room)
+  unsigned long long nbase = 0;
+  if (lane == 0) {
+    if (unused) atomicAdd(c.ctl + kCtlUsed, (unsigned long long)-(long long)__popcll(unused));
+    if (cm) {
+      nbase = atomicAdd(c.ctl + kCtlNew, (unsigned long long)__popcll(cm));
+      atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
+    }
+    if (fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
+    if (xm) {
+      atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
+      atomicExch(c.ctl + kCtlFull, 1ull);
+    }
   }
-  if (lane == 0 && fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
-  if (lane == 0 && xm) {
-    atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
-    atomicExch(c.ctl + kCtlFull, 1ull);
-  }
-  base = __shfl(base, 0);
-  if (claimed) {
-    const uint64_t below = cm & ((1ull << lane) - 1ull);
-    c.new_list[base + (unsigned long long)__popcll(below)] = make_uint2((uint32_t)slot, i);
-  }
+  nbase = __shfl(nbase, 0);
+  if (claimed) c.new_list[nbase + (unsigned long long)__popcll(cm & ((1ull << lane) - 1ull))] = make_uint2((uint32_t)slot, i);
 }
 
 // One lane per entry claimed by this launch: key, dalek decode verdict and [j]A (build_a_table, the verify kernel's own

@@ -47,7 +47,7 @@ typedef struct {
   uint32_t small_batch_max; /* launches of at most this many records run the low-latency kernel (two lanes per
                                record, one wave per SIMD); 0 = 32768; AT2V_SMALL_BATCH_OFF = never */
   uint32_t sender_cache;    /* per-sender A cache (AT2 senders repeat: accounts/account.rs:36-43): capacity in distinct
-                               public keys, 0 = off. A record whose sender A is cached skips decoding A and building
+                               public keys, 0 = off. When full it is cleared and refilled. A record whose sender A is cached skips decoding A and building
                                its [j]A table; the verdict is unchanged (the cache holds only values derived from the
                                32 bytes of A, and every hit is confirmed by comparing those bytes). */
 } at2v_opts;
