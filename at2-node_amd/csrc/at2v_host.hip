@@ -16,10 +16,17 @@
 
 namespace {
 
+// A slot's host buffers are ONE pinned allocation and its device buffers ONE device allocation with the same layout
+// [pk cap x 32 | sig cap x 64 | off (cap + 1) x 4 | msg cap_msg], so a batch whose used span (the record arrays up to
+// the capacity, plus the used message bytes) is small goes up in a single copy instead of four (kSingleCopyMax).
 struct DevSlot {
+  uint8_t* dev = nullptr;  // device allocation
+  uint8_t* host = nullptr; // pinned host allocation (slot.pk points at its start)
+  size_t msg_at = 0;       // byte offset of msg in both allocations
   void *pk = nullptr, *sig = nullptr, *msg = nullptr, *off = nullptr, *ver = nullptr;
   hipEvent_t uploaded = nullptr, verified = nullptr, done = nullptr;
 };
+constexpr size_t kSingleCopyMax = 2u << 20;
 
 struct HipBackend {
   at2v_ctx* ctx = nullptr;
@@ -56,28 +63,36 @@ struct HipBackend {
     if (!d) return AT2V_E_OOM;
     s.backend = d;
     const size_t words = (s.cap_records + 31) / 32;
-    bool ok = hipHostMalloc((void**)&s.pk, s.cap_records * 32, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void**)&s.sig, s.cap_records * 64, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void**)&s.msg, s.cap_msg, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void**)&s.off, (s.cap_records + 1) * 4, hipHostMallocDefault) == hipSuccess &&
+    const size_t cap = s.cap_records;
+    d->msg_at = (cap * 100 + 4 + 15) / 16 * 16;  // pk, sig, off, then msg 16-byte aligned
+    const size_t bytes = d->msg_at + s.cap_msg + 16;
+    bool ok = hipHostMalloc((void**)&d->host, bytes, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void**)&s.verdicts, words * 4, hipHostMallocDefault) == hipSuccess &&
-              hipMalloc(&d->pk, s.cap_records * 32) == hipSuccess && hipMalloc(&d->sig, s.cap_records * 64) == hipSuccess &&
-              hipMalloc(&d->msg, s.cap_msg + 16) == hipSuccess && hipMalloc(&d->off, (s.cap_records + 1) * 4) == hipSuccess &&
-              hipMalloc(&d->ver, words * 4) == hipSuccess &&
-              hipEventCreateWithFlags(&d->uploaded, hipEventDisableTiming) == hipSuccess &&
+              hipMalloc((void**)&d->dev, bytes) == hipSuccess && hipMalloc(&d->ver, words * 4) == hipSuccess;
+    if (ok) {
+      s.pk = d->host;
+      s.sig = d->host + cap * 32;
+      s.off = reinterpret_cast<uint32_t*>(d->host + cap * 96);
+      s.msg = d->host + d->msg_at;
+      d->pk = d->dev;
+      d->sig = d->dev + cap * 32;
+      d->off = d->dev + cap * 96;
+      d->msg = d->dev + d->msg_at;
+    }
+    ok = ok && hipEventCreateWithFlags(&d->uploaded, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&d->verified, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&d->done, hipEventDisableTiming) == hipSuccess;
     return ok ? AT2V_OK : AT2V_E_OOM;
   }
   void release(at2v::QueueSlot& s) {
     (void)hipSetDevice(device);
-    for (void* p : {(void*)s.pk, (void*)s.sig, (void*)s.msg, (void*)s.off, (void*)s.verdicts})
-      if (p) (void)hipHostFree(p);
+    if (s.verdicts) (void)hipHostFree(s.verdicts);
     s.pk = s.sig = s.msg = nullptr;
     s.off = s.verdicts = nullptr;
     DevSlot* d = static_cast<DevSlot*>(s.backend);
     if (!d) return;
-    for (void* p : {d->pk, d->sig, d->msg, d->off, d->ver})
+    if (d->host) (void)hipHostFree(d->host);
+    for (void* p : {(void*)d->dev, d->ver})
       if (p) (void)hipFree(p);
     for (hipEvent_t e : {d->uploaded, d->verified, d->done})
       if (e) (void)hipEventDestroy(e);
@@ -89,10 +104,14 @@ struct HipBackend {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
     hipError_t e = hipSetDevice(device);
     const size_t n = s.n, words = (n + 31) / 32;
-    if (e == hipSuccess) e = hipMemcpyAsync(d->pk, s.pk, n * 32, hipMemcpyHostToDevice, h2d);
-    if (e == hipSuccess) e = hipMemcpyAsync(d->sig, s.sig, n * 64, hipMemcpyHostToDevice, h2d);
-    if (e == hipSuccess && s.msg_used) e = hipMemcpyAsync(d->msg, s.msg, s.msg_used, hipMemcpyHostToDevice, h2d);
-    if (e == hipSuccess) e = hipMemcpyAsync(d->off, s.off, (n + 1) * 4, hipMemcpyHostToDevice, h2d);
+    if (d->msg_at + s.msg_used <= kSingleCopyMax) {  // one copy of the whole used span (small slots / latency mode)
+      if (e == hipSuccess) e = hipMemcpyAsync(d->dev, d->host, d->msg_at + s.msg_used, hipMemcpyHostToDevice, h2d);
+    } else {
+      if (e == hipSuccess) e = hipMemcpyAsync(d->pk, s.pk, n * 32, hipMemcpyHostToDevice, h2d);
+      if (e == hipSuccess) e = hipMemcpyAsync(d->sig, s.sig, n * 64, hipMemcpyHostToDevice, h2d);
+      if (e == hipSuccess && s.msg_used) e = hipMemcpyAsync(d->msg, s.msg, s.msg_used, hipMemcpyHostToDevice, h2d);
+      if (e == hipSuccess) e = hipMemcpyAsync(d->off, s.off, (n + 1) * 4, hipMemcpyHostToDevice, h2d);
+    }
     if (e == hipSuccess) e = hipEventRecord(d->uploaded, h2d);
     if (e == hipSuccess) e = hipStreamWaitEvent(comp, d->uploaded, 0);
     if (e != hipSuccess) return AT2V_E_HIP;
