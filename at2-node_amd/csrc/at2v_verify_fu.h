@@ -19,7 +19,7 @@ namespace at2v {
 // entry) and a_cached_ok is dalek's decode verdict for A; only R is decoded and only R's table is built. Everything the
 // verdict depends on is still a function of (A, R||S, M) alone.
 #ifndef AT2V_PARK_POINTS
-#define AT2V_PARK_POINTS 1  // decoded A and R parked in the table slots across SHA-512 / lattice (0: kept live)
+#define AT2V_PARK_POINTS 0  // 1: decoded A and R parked in the table slots across SHA-512 / lattice (0: kept live)
 #endif
 
 template <bool kCacheable = false, class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax,
