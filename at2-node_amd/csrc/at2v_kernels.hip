@@ -333,14 +333,15 @@ __device__ AT2V_INLINE bool cache_hit(const int4* __restrict__ cache, int slot, 
 // Half-size verification: one chunk of 64 records per wave, no final inversion. kCache: the per-sender A
 // cache is on; a wave whose 64 records all hit it skips decoding A and building [j]A (slot_of / cache from
 // cache_lookup_kernel + cache_build_kernel, launched just before on the same stream).
+// The body is a device function under two kernels with their own parameter lists, so the uncached kernel keeps exactly
+// round 2's signature and code (an extra-parameter template of it measured ~1% slower: profiles/r03b, r03d).
 template <bool kCache>
-__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
-    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
-    const int* __restrict__ slot_of, const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl) {
-  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
-  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+__device__ AT2V_INLINE void verify_chunks(
+    int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
+    uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
+    uint32_t* __restrict__ chunk_queue, const int* __restrict__ slot_of, const int4* __restrict__ cache,
+    unsigned long long* __restrict__ cache_ctl) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
@@ -464,6 +465,28 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   }
 }
 
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  verify_chunks<false>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
+                       nullptr, nullptr, nullptr);
+}
+
+// the same with the per-sender A cache (at2v_opts.sender_cache)
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_cached(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
+    const int* __restrict__ slot_of, const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
+                      slot_of, cache, cache_ctl);
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // Low-latency verify for small launches: two lanes per record (lane 2r: A side, lane 2r+1: R side,
 // verify_pair_part), 32 records per wave, one wave per SIMD (4-wave blocks, 80 KiB LDS). Each lane decodes one point,
@@ -532,12 +555,10 @@ __global__ __launch_bounds__(kPairBlock, 1) void verify_pair_kernel(
   }
 }
 #else
-template <bool kCache>  // the cache applies to the half-size kernel only; here for a common launcher signature
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
-    const int* __restrict__, const int4* __restrict__, unsigned long long* __restrict__) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 bstage[kWavesPerBlock * 8 * 64];
   const int lane = threadIdx.x & 63;
@@ -1043,13 +1064,13 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   if (cache) {
     const hipError_t ce = launch_cache_prepare(*cache, pk, n, stream);
     if (ce != hipSuccess) return ce;
-    hipLaunchKernelGGL(verify_kernel<true>, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+    hipLaunchKernelGGL(verify_kernel_cached, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
                        verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL(verify_kernel<false>, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                     verdicts, scratch, btab, queue, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+                     verdicts, scratch, btab, queue);
   return hipGetLastError();
 }
 
@@ -1076,10 +1097,10 @@ hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStrea
 }
 
 hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs) {
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, verify_kernel<false>, kBlock, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, verify_kernel, kBlock, 0);
   if (e != hipSuccess) return e;
   hipFuncAttributes attr;
-  e = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(verify_kernel<false>));
+  e = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(verify_kernel));
   if (e == hipSuccess && vgprs) *vgprs = attr.numRegs;
   return e;
 }
