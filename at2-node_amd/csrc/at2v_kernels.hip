@@ -360,6 +360,9 @@ __device__ AT2V_INLINE void verify_chunks(
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t nwords = (n + 31) / 32;
+#ifndef AT2V_MSG_TOUCH
+#define AT2V_MSG_TOUCH 1  // early loads of each lane's message sectors (consumed at SHA-512), see verify_chunks
+#endif
 #ifndef AT2V_EXP_SLOT_WAVES
 #define AT2V_EXP_SLOT_WAVES 0  // EXPERIMENT ONLY (wrong verdicts): > 0 = waves share AT2V_EXP_SLOT_WAVES table slots, so the
                                // tables' footprint is L2-resident; measures what the table traffic costs in time/clock
@@ -416,8 +419,8 @@ __device__ AT2V_INLINE void verify_chunks(
         __builtin_amdgcn_readfirstlane(__all((uint64_t)o0 + len + 8 <= (uint64_t)msg_total) ? 1 : 0);
     const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (o0 >> 2);
     const uint32_t msh = (o0 & 3u) * 8;
-    auto msgword = [&](uint32_t j) -> uint32_t {
-      if (msg_fast) return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh);
+    auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
+    auto msg_guarded = [=](uint32_t j) -> uint32_t {
       const uint32_t a = o0 + 4 * j;
       const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
       const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
@@ -425,6 +428,22 @@ __device__ AT2V_INLINE void verify_chunks(
       const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
       return __builtin_amdgcn_alignbit(hi, lo, sh);
     };
+#if AT2V_MSG_TOUCH
+    // Touch the first three 64-byte sectors of the lane's message now, so SHA-512 (after the two decodes) finds them in
+    // cache: its message loads are issued one at a time, each behind its own wait. The words are consumed by an empty asm
+    // statement at the start of SHA-512 (so the loads are kept and their wait lands there, long after they returned).
+    uint32_t touch[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const uint32_t a = o0 + (64u * q < len ? 64u * q : (len ? len - 1 : 0u));
+      touch[q] = msg_total ? *reinterpret_cast<const uint32_t*>(msg + ((a < msg_total ? a : msg_total - 1) & ~3u)) : 0u;
+    }
+    auto touched = [=]() { asm volatile("" ::"v"(touch[0]), "v"(touch[1]), "v"(touch[2])); };
+#else
+    auto touched = [] {};
+#endif
+    MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> msgword{msg_fast, msg_unguarded,
+                                                                                        msg_guarded, touched};
 #if AT2V_FIELD_FU
     int good;
     if (kCache) {
@@ -946,7 +965,24 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
       }
     }
   }
-  // reserve the wave's claims against the capacity
+  // Lanes of this wave that want to claim the same key elect one leader (the lowest lane): AT2 traffic puts many records
+  // of one sender in a wave, and reserving once per record would exhaust the capacity with duplicates. One iteration
+  // per distinct wanted key in the wave.
+  int leader = lane;
+  {
+    uint64_t pending = __ballot(want);
+    while (pending) {
+      const int L = __ffsll((long long)pending) - 1;
+      const uint64_t fpL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fp >> 32), L) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fp, L);
+      const int same = want && fp == fpL;
+      if (same) leader = L;
+      pending &= ~__ballot(same);
+    }
+  }
+  const int follower = want && leader != lane;
+  want = want && !follower;
+  // reserve the wave's claims (one per distinct key) against the capacity
   const uint64_t wm = __ballot(want);
   unsigned long long base = 0;
   if (lane == 0 && wm) base = atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(wm));
@@ -969,7 +1005,14 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
       }
     }
   }
-  if (denied) {  // phase 3: a lane of this wave with the same key may have claimed it meanwhile (same probe path)
+  {  // followers take their leader's outcome (a shuffle: every lane of the wave takes part)
+    const int ls = __shfl(slot, leader);
+    if (follower) {
+      slot = ls;
+      found = ls >= 0;
+    }
+  }
+  if (denied || (follower && slot < 0)) {  // phase 3: another wave may have claimed the key meanwhile (same probe path)
     for (uint32_t q = 0; q < 32; ++q) {
       const uint32_t j = (h + q) & mask;
       const unsigned long long t = __hip_atomic_load(c.tags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

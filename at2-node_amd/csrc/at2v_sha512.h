@@ -184,4 +184,33 @@ AT2V_HD AT2V_INLINE void sha512_prefixed(uint64_t h[8], const uint32_t* prefix, 
   }
 }
 
+// A message source that chooses, once per wave, between an unguarded reader (every lane's message ends well before the
+// buffer end) and a bounds-checked one. Each SHA-512 instantiation is then straight-line code whose message loads the
+// compiler can issue back to back; a wave-uniform branch per word between the two readers kept every load behind its
+// own s_waitcnt (one memory latency per message word, ~26 per signature at 100-byte messages).
+struct MsgNoTouch {
+  AT2V_HD AT2V_INLINE void operator()() const {}
+};
+template <class Fast, class Slow, class Touch = MsgNoTouch>
+struct MsgSplit {
+  int fast;
+  Fast f;
+  Slow s;
+  Touch touch;  // called once before the hash: consumes the kernel's early loads of the message (AT2V_MSG_TOUCH)
+};
+
+template <int NPW, class MsgWord>
+AT2V_HD AT2V_INLINE void sha512_msg(uint64_t h[8], const uint32_t* prefix, uint32_t len, MsgWord& m) {
+  sha512_prefixed<NPW>(h, prefix, len, m);
+}
+template <int NPW, class Fast, class Slow, class Touch>
+AT2V_HD AT2V_INLINE void sha512_msg(uint64_t h[8], const uint32_t* prefix, uint32_t len,
+                                    MsgSplit<Fast, Slow, Touch>& m) {
+  m.touch();
+  if (m.fast)
+    sha512_prefixed<NPW>(h, prefix, len, m.f);
+  else
+    sha512_prefixed<NPW>(h, prefix, len, m.s);
+}
+
 }  // namespace at2v

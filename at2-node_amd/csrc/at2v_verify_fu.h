@@ -65,7 +65,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
       pre[8 + i] = Aw[i];
     }
     uint64_t h[8];
-    sha512_prefixed<16>(h, pre, len, msgword);
+    sha512_msg<16>(h, pre, len, msgword);
     uint32_t hw[16];
     sha512_digest_words(hw, h);
     sc_reduce512(k, hw);
@@ -282,7 +282,7 @@ AT2V_HD AT2V_INLINE int verify_pair_part(int side, const uint32_t Rw[8], const u
       pre[8 + i] = Aw[i];
     }
     uint64_t h[8];
-    sha512_prefixed<16>(h, pre, len, msgword);
+    sha512_msg<16>(h, pre, len, msgword);
     uint32_t hw[16];
     sha512_digest_words(hw, h);
     sc_reduce512(k, hw);
