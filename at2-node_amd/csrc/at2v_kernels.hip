@@ -361,7 +361,7 @@ __device__ AT2V_INLINE void verify_chunks(
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t nwords = (n + 31) / 32;
 #ifndef AT2V_MSG_TOUCH
-#define AT2V_MSG_TOUCH 1  // early loads of each lane's message sectors (consumed at SHA-512), see verify_chunks
+#define AT2V_MSG_TOUCH 0  // 1: early loads of each lane's message sectors (consumed at SHA-512), see verify_chunks
 #endif
 #ifndef AT2V_EXP_SLOT_WAVES
 #define AT2V_EXP_SLOT_WAVES 0  // EXPERIMENT ONLY (wrong verdicts): > 0 = waves share AT2V_EXP_SLOT_WAVES table slots, so the
