@@ -175,6 +175,26 @@ def pack_records(pks: Sequence[bytes], sigs: Sequence[bytes], msgs: Sequence[byt
     return pk, sig, msg, off
 
 
+def launch_streams(count: int = 2, device: Optional[int] = None) -> list:
+    """`count` non-blocking HIP streams (hipStreamCreateWithFlags) on `device` (current if None), as
+    torch.cuda.ExternalStream objects. Verify launches alternating over them overlap: the context's scratch sets let
+    launch k+1 take the CUs launch k leaves during its end-of-launch drain (at2v_api.hip). Each stream the runtime
+    creates gets its own hardware queue in turn, which is what lets the two kernels run side by side."""
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    out = []
+    with torch.cuda.device(torch.cuda.current_device() if device is None else device):
+        for _ in range(count):
+            h = ctypes.c_void_p()
+            rc = hip.hipStreamCreateWithFlags(ctypes.byref(h), 1)  # hipStreamNonBlocking
+            if rc != 0:
+                raise At2vError(-3, f"hipStreamCreateWithFlags failed ({rc})")
+            out.append(torch.cuda.ExternalStream(h.value))
+    return out
+
+
 class BatchVerifier:
     """Owns an at2v context (one or more gfx950 devices)."""
 

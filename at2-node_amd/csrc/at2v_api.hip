@@ -5,9 +5,12 @@
 // (aligned to 64 records = one wave chunk = two verdict words) across the context's devices;
 // each shard runs H2D -> verify -> D2H on its own stream, so shards overlap.
 //
-// Every verify launch of a context goes through launch_shard(): launches take turns on the device's
-// scratch (an event recorded after each launch, waited on by the next one, whatever stream either is on),
-// and the verdict words are zeroed before the kernel, so a chunk that no wave wrote fails closed.
+// Every verify launch of a context goes through launch_shard(). A device has kScratchSets scratch sets (per-wave tables,
+// chunk-queue counter, pacing lines) used in turn: a launch waits only for the launch that last used its set (an event,
+// whatever stream that ran on), so launches on DIFFERENT caller streams overlap: the next batch's blocks take the CUs the
+// previous launch's last blocks leave, instead of the device idling through its end-of-launch drain (+3.6% on
+// back-to-back config-2 batches, profiles/r03i). The verdict words are zeroed before the kernel, so a chunk that no wave
+// wrote fails closed.
 //
 // Multi-process (one rank per GPU): at2v_comm_init_rank attaches an RCCL communicator to a
 // context; at2v_verify_shard_gather_device / at2v_verify_batch_sharded verify this rank's index range and
@@ -72,21 +75,28 @@ struct DevBuf {
 // the counters' asynchronous copy and clears the tags before a later launch (eviction = start over).
 struct SenderCache {
   at2v::CacheArgs args{};
+  hipEvent_t free = nullptr;  // recorded after every cached launch: cached launches never overlap (shared tags/slots)
   DevBuf tags, entries, slot_of, new_list, ctl;
   unsigned long long* host_ctl = nullptr;  // pinned copy of the device counters, refreshed after every cached launch
   hipEvent_t ctl_copied = nullptr;
   bool copy_pending = false;
 };
 
+// scratch sets per device (AT2V_SCRATCH_SETS overrides, 1..4; 1 = every launch waits for the previous one)
+constexpr int kScratchSets = 2;
+
 struct Shard {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t scratch_free = nullptr;  // recorded after every verify launch: the next one waits on it
+  int sets = kScratchSets;
+  unsigned next_set = 0;
+  hipEvent_t scratch_free[4] = {};  // per set: recorded after the launch that last used it; the set's next launch waits
   int grid = 0;  // persistent grid (blocks)
   int cus = 0;
   int blocks_per_cu = 0;
   int vgprs = 0;
-  DevBuf scratch, btab, pk, sig, msg, off, verdict;
+  DevBuf scratch[4];
+  DevBuf btab, pk, sig, msg, off, verdict;
   SenderCache* cache = nullptr;
 };
 
@@ -134,9 +144,12 @@ int init_shard(Shard& s, int device) {
   if (s.blocks_per_cu < 1) s.blocks_per_cu = 1;
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-  AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free, hipEventDisableTiming));
-  AT2V_TRY(hipEventRecord(s.scratch_free, s.stream));
-  AT2V_TRY(s.scratch.ensure(at2v::scratch_bytes(s.grid)));
+  if (const char* v = std::getenv("AT2V_SCRATCH_SETS")) s.sets = std::min(4, std::max(1, std::atoi(v)));
+  for (int j = 0; j < s.sets; ++j) {
+    AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free[j], hipEventDisableTiming));
+    AT2V_TRY(hipEventRecord(s.scratch_free[j], s.stream));
+    AT2V_TRY(s.scratch[j].ensure(at2v::scratch_bytes(s.grid)));
+  }
   // fixed-base table [0..2^(AT2V_BWIN-1)]B, built on the device once per context
   AT2V_TRY(s.btab.ensure(at2v::btab_bytes()));
   AT2V_TRY(at2v::launch_build_btab((int4*)s.btab.p, s.stream));
@@ -155,6 +168,7 @@ void free_cache(SenderCache*& c) {
   c->ctl.release();
   if (c->host_ctl) (void)hipHostFree(c->host_ctl);
   if (c->ctl_copied) (void)hipEventDestroy(c->ctl_copied);
+  if (c->free) (void)hipEventDestroy(c->free);
   delete c;
   c = nullptr;
 }
@@ -185,6 +199,8 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed) {
   AT2V_TRY(hipHostMalloc((void**)&c->host_ctl, c->ctl.cap, hipHostMallocDefault));
   std::memset(c->host_ctl, 0, c->ctl.cap);
   AT2V_TRY(hipEventCreateWithFlags(&c->ctl_copied, hipEventDisableTiming));
+  AT2V_TRY(hipEventCreateWithFlags(&c->free, hipEventDisableTiming));
+  AT2V_TRY(hipEventRecord(c->free, s.stream));
   c->args.tags = (unsigned long long*)c->tags.p;
   c->args.entries = (int4*)c->entries.p;
   c->args.ctl = (unsigned long long*)c->ctl.p;
@@ -211,26 +227,30 @@ hipError_t cache_before_launch(SenderCache& c, uint32_t n, hipStream_t stream) {
   return e;
 }
 
-// One verify launch on shard s (current device = s.device), on `stream`. Launches of a context take turns
-// on the shard's scratch (per-wave tables, chunk-queue counter, pacing lines): this one waits for the
-// previous one, on whatever stream that ran. The verdict words are zeroed first (fail closed).
+// One verify launch on shard s (current device = s.device), on `stream`. The launch takes the shard's next scratch set
+// and waits for the launch that last used that set, on whatever stream that ran; launches on different streams may
+// therefore run concurrently (on one stream they are ordered anyway). Cached launches also wait for the previous cached
+// launch (the cache's tags and per-launch slot arrays are shared). The verdict words are zeroed first (fail closed).
 hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                         uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream,
                         bool zero_verdicts = true) {
-  hipError_t e = hipStreamWaitEvent(stream, s.scratch_free, 0);
+  const int j = (int)(s.next_set++ % (unsigned)s.sets);
+  hipError_t e = hipStreamWaitEvent(stream, s.scratch_free[j], 0);
   if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
   // the cache serves the throughput kernel (launches above small_batch_max records)
   SenderCache* c = (s.cache && n > ctx->pair_max) ? s.cache : nullptr;
+  if (e == hipSuccess && c) e = hipStreamWaitEvent(stream, c->free, 0);
   if (e == hipSuccess && c) e = cache_before_launch(*c, n, stream);
   if (e == hipSuccess)
-    e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch.p,
+    e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch[j].p,
                             (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &c->args : nullptr);
   if (e == hipSuccess && c) {
     e = hipMemcpyAsync(c->host_ctl, c->ctl.p, c->ctl.cap, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipEventRecord(c->ctl_copied, stream);
     c->copy_pending = e == hipSuccess;
+    if (e == hipSuccess) e = hipEventRecord(c->free, stream);
   }
-  if (e == hipSuccess) e = hipEventRecord(s.scratch_free, stream);
+  if (e == hipSuccess) e = hipEventRecord(s.scratch_free[j], stream);
   return e;
 }
 
@@ -257,6 +277,10 @@ int gather_shard(at2v_ctx* ctx, Shard& s, int local, const uint8_t* d_pk, const 
   if (ez != hipSuccess && ctx->zeros.ensure(wpr * 4) == hipSuccess &&
       hipMemset(ctx->zeros.p, 0, ctx->zeros.cap) == hipSuccess)
     send = ctx->zeros.p;
+  // Collectives of one communicator run one at a time in issue order on every rank: a caller that alternates streams
+  // (so that consecutive verify launches overlap) must not let two all-gathers run concurrently, or ranks could
+  // execute them in different orders. This one waits for the previous one, whatever stream it ran on.
+  if (ctx->gather_done) (void)hipStreamWaitEvent(st, ctx->gather_done, 0);
   // in place when send == recvbuff + rank * count
   const ncclResult_t r = ncclAllGather(send, d_bitmap, wpr, ncclUint32, ctx->comm, st);
   ++ctx->gathers;
@@ -309,7 +333,8 @@ void at2v_destroy(at2v_ctx* ctx) {
   for (Shard& s : ctx->shards) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (s.scratch_free) (void)hipEventSynchronize(s.scratch_free);
+    for (hipEvent_t ev : s.scratch_free)
+      if (ev) (void)hipEventSynchronize(ev);
   }
   if (ctx->comm) {
     (void)hipSetDevice(ctx->shards.empty() ? 0 : ctx->shards[0].device);
@@ -324,9 +349,10 @@ void at2v_destroy(at2v_ctx* ctx) {
   ctx->status.release();
   for (Shard& s : ctx->shards) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
-    if (s.scratch_free) (void)hipEventDestroy(s.scratch_free);
+    for (hipEvent_t ev : s.scratch_free)
+      if (ev) (void)hipEventDestroy(ev);
     free_cache(s.cache);
-    s.scratch.release();
+    for (DevBuf& b : s.scratch) b.release();
     s.btab.release();
     s.pk.release();
     s.sig.release();
@@ -434,7 +460,10 @@ int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BY
   if (rc == AT2V_OK) rc = hip_code(hipMemset(ctx->zeros.p, 0, ctx->zeros.cap));
   if (rc == AT2V_OK) rc = hip_code(ctx->window.ensure(kGatherWindow * 4 * (size_t)world));
   if (rc == AT2V_OK) rc = hip_code(ctx->status.ensure(4));
-  if (rc == AT2V_OK && !ctx->gather_done) rc = hip_code(hipEventCreateWithFlags(&ctx->gather_done, hipEventDisableTiming));
+  if (rc == AT2V_OK && !ctx->gather_done) {
+    rc = hip_code(hipEventCreateWithFlags(&ctx->gather_done, hipEventDisableTiming));
+    if (rc == AT2V_OK) rc = hip_code(hipEventRecord(ctx->gather_done, ctx->shards[0].stream));  // first wait: no-op
+  }
   // collective: blocks until all `world` ranks have called it (a rank that failed above still joins, then reports)
   const int rn = nccl_code(ncclCommInitRank(&ctx->comm, world, id, rank));
   if (rn == AT2V_OK && ctx->status.p) {

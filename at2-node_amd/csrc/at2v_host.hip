@@ -1,7 +1,8 @@
 // at2v_host.hip — C ABI of the host-side pieces around the verify kernel (include/at2v.h):
-//   * at2v_queue_*   ingest/batching queue (at2v_queue.h) over a HIP backend: pinned host slots, one
-//                    stream each for H2D copies, verify kernels and D2H copies, so batch k+1 uploads while
-//                    batch k verifies (kernels themselves serialise: they share the context's scratch);
+//   * at2v_queue_*   ingest/batching queue (at2v_queue.h) over a HIP backend: pinned host slots, one stream for
+//                    H2D copies, two alternating verify streams and one for D2H copies, so batch k+1 uploads while
+//                    batch k verifies, and batch k+1's kernel fills the CUs batch k's kernel leaves at its end (the
+//                    context's scratch sets, at2v_api.hip);
 //   * at2v_pack_*    SendAssetRequest -> verify records (at2v_pack.h);
 //   * at2v_ledger_*  accounts / recent transactions / apply loop (at2v_ledger.h).
 #include <hip/hip_runtime.h>
@@ -31,7 +32,8 @@ constexpr size_t kSingleCopyMax = 2u << 20;
 struct HipBackend {
   at2v_ctx* ctx = nullptr;
   int device = 0;
-  hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+  hipStream_t h2d = nullptr, comp[2] = {nullptr, nullptr}, d2h = nullptr;
+  unsigned launches = 0;
 
   int init(const at2v_queue_opts& o) {
     at2v_opts co{o.device, 1, o.policy};
@@ -40,13 +42,14 @@ struct HipBackend {
     device = o.device;
     if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
     if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
-    if (hipStreamCreateWithFlags(&comp, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
+    for (hipStream_t& c : comp)
+      if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     if (hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     return AT2V_OK;
   }
   void fini() {
     if (hipSetDevice(device) == hipSuccess) {
-      for (hipStream_t* s : {&h2d, &comp, &d2h})
+      for (hipStream_t* s : {&h2d, &comp[0], &comp[1], &d2h})
         if (*s) {
           (void)hipStreamSynchronize(*s);
           (void)hipStreamDestroy(*s);
@@ -99,9 +102,10 @@ struct HipBackend {
     delete d;
     s.backend = nullptr;
   }
-  // H2D on h2d -> verify on comp (waits for its upload) -> D2H on d2h (waits for its kernel)
+  // H2D on h2d -> verify on comp[k % 2] (waits for its upload) -> D2H on d2h (waits for its kernel)
   int launch(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
+    hipStream_t comp = this->comp[launches++ & 1];
     hipError_t e = hipSetDevice(device);
     const size_t n = s.n, words = (n + 31) / 32;
     if (d->msg_at + s.msg_used <= kSingleCopyMax) {  // one copy of the whole used span (small slots / latency mode)

@@ -6,7 +6,8 @@ Workload (BASELINE config 2, weak-scaled): every rank verifies its own batch of 
 RFC 8032 generator and resident in HBM before timing starts. One step = one verify
 launch over the rank's batch + (N > 1) one RCCL all-gather of the verdict bitmap words over xGMI, both
 inside libat2v (at2v_verify_shard_gather_device). Config 3 (16M over 8 GPUs) = `--records-per-gpu 2097152`
-at N = 8.
+at N = 8. Steps alternate over two HIP launch streams, so step k+1's kernel fills the CUs that step k's kernel
+leaves during its end-of-launch drain, as consecutive batches of a running node do.
 
 Launch: `python bench.py --gpus N` starts its own N rank processes (children, one per GPU) when it is not
 already under torch.distributed.run; under torch.distributed.run each process is one rank.
@@ -196,23 +197,30 @@ def main():
         v.comm_init_rank(uid[0], rank, world)
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
+    # Steps alternate over two launch streams (their own hardware queues): step k+1's kernel fills the CUs step k's
+    # kernel leaves during its end-of-launch drain (the library gives each in-flight launch its own scratch set).
+    lstreams = at2v.launch_streams(2, local)
     d_pk = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     d_sig = torch.empty(n * 64, dtype=torch.uint8, device=dev)
     d_msg = torch.empty(n * L, dtype=torch.uint8, device=dev)
     d_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
     words = n // 32
-    d_ver = torch.zeros(words, dtype=torch.int32, device=dev)
-    d_all = torch.zeros(words * world, dtype=torch.int32, device=dev)  # node bitmap (N > 1)
+    # one verdict bitmap per launch stream, so overlapping steps never write the same words
+    d_vers = [torch.zeros(words, dtype=torch.int32, device=dev) for _ in lstreams]
+    d_alls = [torch.zeros(words * world, dtype=torch.int32, device=dev) for _ in lstreams]  # node bitmaps (N > 1)
+    d_ver, d_all = d_vers[0], d_alls[0]
     # distinct records per rank (indices rank*n .. rank*n+n-1)
     v.gen_records_device(CFG_SEED, rank * n, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
                          d_off.data_ptr(), s, senders=args.senders)
     torch.cuda.synchronize(dev)
 
-    def verify(pk, sig, msg, off, strm):
+    def verify(pk, sig, msg, off, j):
+        """one step on launch stream j (its own verdict bitmap)"""
+        strm = lstreams[j].cuda_stream
         if use_dist:  # verify this rank's shard into its slice of the node bitmap, then RCCL all-gather
-            v.verify_shard_gather_device(pk, sig, msg, n * L, off, n, words, d_all.data_ptr(), strm)
+            v.verify_shard_gather_device(pk, sig, msg, n * L, off, n, words, d_alls[j].data_ptr(), strm)
         else:
-            v.verify_batch_device(pk, sig, msg, n * L, off, n, d_ver.data_ptr(), strm)
+            v.verify_batch_device(pk, sig, msg, n * L, off, n, d_vers[j].data_ptr(), strm)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -227,29 +235,44 @@ def main():
         return t.tolist()
 
     ptrs = (d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr())
-    for _ in range(args.warmup):
-        verify(*ptrs, s)
+    for k in range(args.warmup):
+        verify(*ptrs, k % 2)
     barrier()
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the launch streams: one start (both streams wait for it) and one end per step, recorded on that
+    # step's stream right after its launch. Device time per step = (last end - start) / K: the period of the
+    # overlapped launches, i.e. the device-side throughput of the timed region.
+    ev0 = torch.cuda.Event(enable_timing=True)
+    kend = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
+    ev0.record(lstreams[0])
+    lstreams[1].wait_event(ev0)
     for k in range(args.steps):
-        kev[k][0].record(stream)
-        verify(*ptrs, s)
-        kev[k][1].record(stream)
+        verify(*ptrs, k % 2)
+        kend[k].record(lstreams[k % 2])
     barrier()
     elapsed = time.perf_counter() - t0
-    # device time per step on the launch stream: the verify kernel (N = 1) or kernel + all-gather (N > 1)
-    kernel_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps
-    elapsed, kernel_ms = reduce([elapsed, kernel_ms], dist.ReduceOp.MAX if use_dist else None)
+    # device time per step on the launch streams: the verify kernels (N = 1) or kernels + all-gathers (N > 1)
+    kernel_ms = max(ev0.elapsed_time(e) for e in kend) / args.steps
+    # one launch alone (nothing before or after it on the device): its duration is what a kernel-trace profile of a
+    # single launch reports; the timed steps overlap by up to the end-of-launch drain
+    ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ea.record(lstreams[0])
+    verify(*ptrs, 0)
+    eb.record(lstreams[0])
+    barrier()
+    launch_ms_alone = ea.elapsed_time(eb)
+    elapsed, kernel_ms, launch_ms_alone = reduce([elapsed, kernel_ms, launch_ms_alone],
+                                                 dist.ReduceOp.MAX if use_dist else None)
 
     # verdict check after the timed region: every generated record must be valid, on every rank (N > 1: the
-    # gathered node bitmap, all ranks' records)
-    full = d_all if use_dist else d_ver
-    match = float((full == -1).float().mean().item())
+    # gathered node bitmaps, all ranks' records), in the bitmap of every launch stream the steps used
+    used = d_alls if use_dist else d_vers
+    used = used[: min(2, max(1, args.steps + args.warmup))]
+    match = min(float((full == -1).float().mean().item()) for full in used)
     match = reduce([match], dist.ReduceOp.MIN)[0] if use_dist else match
 
-    e2e = host_path(args, v, verify, barrier, reduce, dist, torch, dev, stream, d_pk, d_sig, d_msg, d_off, d_ver,
-                    d_all, n, L, words, use_dist, world) if args.e2e else None
+    e2e = host_path(args, v, verify, barrier, reduce, dist, torch, dev, lstreams, d_pk, d_sig, d_msg, d_off, d_vers,
+                    d_alls, n, L, words, use_dist, world) if args.e2e else None
 
     total = n * world * args.steps
     value = total / elapsed
@@ -293,6 +316,11 @@ def main():
             },
             "verdict_match": match,
             "kernel_ms": kernel_ms,
+            "launch_ms_alone": launch_ms_alone,
+            "launch_overlap": "steps alternate over two HIP streams (own hardware queues); each in-flight launch has "
+                              "its own scratch set, so step k+1's blocks take the CUs step k's last blocks leave. "
+                              "kernel_ms = device time per step over the timed region (HIP events); launch_ms_alone = "
+                              "one launch with the device otherwise idle",
             "effective_clock_ghz": None,
             "kernel": {"grid_blocks": info["grid_blocks"], "block": info["block_threads"],
                        "waves_per_cu": info["waves_per_cu"], "vgprs": info["vgprs"]},
@@ -370,17 +398,18 @@ def dry_run(args, rank, world, use_dist, dist, torch, np):
             "unique_id_shared": bool(t[1].item()), "valid": int(want.sum())}
 
 
-def host_path(args, v, verify, barrier, reduce, dist, torch, dev, stream, d_pk, d_sig, d_msg, d_off, d_ver, d_all, n, L,
-              words, use_dist, world):
+def host_path(args, v, verify, barrier, reduce, dist, torch, dev, lstreams, d_pk, d_sig, d_msg, d_off, d_vers, d_alls,
+              n, L, words, use_dist, world):
     """End to end from pinned host buffers: per step H2D of the rank's records, verify (+ the RCCL
     all-gather at N > 1), D2H of the verdict bitmap.
       serial:    the three in order on one stream (what at2v_verify_batch does per call);
-      pipelined: two device input sets, uploads on a copy stream, so batch k+1 uploads while batch k verifies
-                 (what the ingest queue does); the D2H of each bitmap follows its verify.
+      pipelined: two device input sets, uploads on a copy stream, so batch k+1 uploads while batch k verifies,
+                 verifies alternating over the two launch streams (what the ingest queue does); the D2H of each
+                 bitmap follows its verify.
     Whole-job rates (all ranks' records / MAX over ranks of the wall time)."""
     h = [t.cpu().pin_memory() for t in (d_pk, d_sig, d_msg, d_off)]
-    bitmap = d_all if use_dist else d_ver
-    h_out = torch.empty(bitmap.numel(), dtype=torch.int32).pin_memory()
+    bitmaps = d_alls if use_dist else d_vers
+    h_outs = [torch.empty(b.numel(), dtype=torch.int32).pin_memory() for b in bitmaps]
     sets = [[torch.empty_like(t) for t in (d_pk, d_sig, d_msg, d_off)] for _ in range(2)]
     copy = torch.cuda.Stream(dev)
     steps = max(1, args.steps)
@@ -393,31 +422,35 @@ def host_path(args, v, verify, barrier, reduce, dist, torch, dev, stream, d_pk, 
     def run(pipelined):
         up = [torch.cuda.Event() for _ in range(2)]
         free = [torch.cuda.Event() for _ in range(2)]
-        for e in free:
-            e.record(stream)
+        for j, e in enumerate(free):
+            e.record(lstreams[j])
+        for o in h_outs:
+            o.zero_()
         barrier()
         t0 = time.perf_counter()
         for k in range(steps):
-            b = sets[k % 2] if pipelined else sets[0]
+            j = k % 2 if pipelined else 0
+            b = sets[j]
+            stream = lstreams[j]
             if pipelined:
-                copy.wait_event(free[k % 2])
+                copy.wait_event(free[j])
                 upload(b, copy)
-                up[k % 2].record(copy)
-                stream.wait_event(up[k % 2])
+                up[j].record(copy)
+                stream.wait_event(up[j])
             else:
                 upload(b, stream)
-            verify(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), b[3].data_ptr(), stream.cuda_stream)
-            free[k % 2].record(stream)
+            verify(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), b[3].data_ptr(), j)
+            free[j].record(stream)
             with torch.cuda.stream(stream):
-                h_out.copy_(bitmap, non_blocking=True)
+                h_outs[j].copy_(bitmaps[j], non_blocking=True)
             if not pipelined:
                 stream.synchronize()
         barrier()
         dt = reduce([time.perf_counter() - t0], dist.ReduceOp.MAX if use_dist else None)[0]
-        ok = bool((h_out == -1).all())
+        ok = all(bool((h_outs[j] == -1).all()) for j in range(2 if pipelined and steps > 1 else 1))
         return n * world * steps / dt, ok
 
-    upload(sets[1], stream)  # warm both sets
+    upload(sets[1], lstreams[0])  # warm both sets
     serial, ok1 = run(False)
     piped, ok2 = run(True)
     return {"e2e_verifies_per_s": piped, "e2e_serial_verifies_per_s": serial,

@@ -1,8 +1,8 @@
 """GPU: the boundary pieces added in round 2, through the C ABI of libat2v.so on a gfx950 —
   * the RCCL rank API (at2v_comm_init_rank, at2v_verify_shard_gather_device, at2v_verify_batch_sharded) at world 1
     (one GPU per rank; a second rank would need a second GPU), against the oracle;
-  * launches of one context on two streams take turns on the scratch and verdict words are zeroed
-    before each kernel;
+  * launches of one context on two streams overlap on separate scratch sets, and verdict words are zeroed before
+    each kernel;
   * at2v_verify_one (CPU) next to the kernel on the same records;
   * BASELINE config 5: a bounded 4-node mini network (tools/mininode.py) with forged copies, identical ledgers.
 Reference anchors: rpc.rs:156-173 (the apply step the gathered bitmap feeds), rpc.rs:275-284 (payload ingest)."""
@@ -100,25 +100,34 @@ def test_rccl_world1_local_failure_still_joins_gather(at2v_mod, oracle):
         assert np.array_equal(got, oracle.verify_batch(pk, sig, msg, off)) and v.info()["gathers"] == g0 + 3
 
 
-def test_two_streams_take_turns_on_scratch(at2v_mod, oracle):
-    """launches of one context on different streams used to share the chunk-queue counter
-    and per-wave tables while both were in flight. Now each waits for the previous; verdict words start zeroed."""
+def test_launches_on_two_streams_overlap_safely(at2v_mod, oracle):
+    """Launches of one context on different streams run concurrently (each in-flight launch takes its own scratch set,
+    so launch k+1 fills the CUs launch k leaves during its drain; at2v_api.hip). Round 1 made them take
+    turns on ONE scratch; now the sets must keep concurrent launches apart: two different batches, one large (the
+    throughput kernel) and one small (the low-latency kernel, same scratch sets), six launches alternating over two
+    hardware-queue streams with nothing synchronised in between, every output compared with the oracle. Verdict words
+    start zeroed (outputs pre-filled with -1)."""
     import torch
-    n, L = 300_000, 64
-    pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 8, 0, n, L)
-    want = oracle.verify_batch(pk, sig, msg, off)
-    dev = "cuda:0"
-    d = [torch.from_numpy(a.reshape(-1).copy()).to(dev) for a in (pk, sig, msg)]
-    d_off = torch.from_numpy(off.view(np.int32).copy()).to(dev)
-    outs = [torch.full(((n + 31) // 32,), -1, dtype=torch.int32, device=dev) for _ in range(4)]
-    streams = [torch.cuda.Stream() for _ in range(2)]
+    L = 64
+    batches = []
+    for seed, n in ((CFG_SEED + 8, 300_000), (CFG_SEED + 9, 5_000)):
+        pk, sig, msg, off, cls = oracle.gen_adversarial(seed, 0, n, L)
+        dev = "cuda:0"
+        d = [torch.from_numpy(a.reshape(-1).copy()).to(dev) for a in (pk, sig, msg)]
+        d_off = torch.from_numpy(off.view(np.int32).copy()).to(dev)
+        batches.append((n, d, d_off, oracle.verify_batch(pk, sig, msg, off)))
+    order = [0, 1, 0, 0, 1, 0]
+    outs = [torch.full(((batches[b][0] + 31) // 32,), -1, dtype=torch.int32, device="cuda:0") for b in order]
+    streams = at2v_mod.launch_streams(2)
     torch.cuda.synchronize()
     with at2v_mod.BatchVerifier(device=0) as v:
-        for k, o in enumerate(outs):  # back to back, alternating streams, nothing synchronised in between
+        for k, (b, o) in enumerate(zip(order, outs)):
+            n, d, d_off, _ = batches[b]
             v.verify_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), n * L, d_off.data_ptr(), n,
                                   o.data_ptr(), streams[k % 2].cuda_stream)
         torch.cuda.synchronize()
-    for o in outs:
+    for b, o in zip(order, outs):
+        n, _, _, want = batches[b]
         got = at2v_mod.unpack_verdicts(o.cpu().numpy().view(np.uint32), n)
         assert np.array_equal(got, want)
 
