@@ -52,13 +52,14 @@ class VerifyError(Exception):
     """Signature rejected (drop::crypto::sign::VerifyError)."""
 
 
-ABI_VERSION = 3  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
+ABI_VERSION = 4  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
 E_PEER = -7      # AT2V_E_PEER: another rank of the communicator failed this collective batch
 
 
 class _Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int),
-                ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32)]
+                ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32),
+                ("sender_comb", ctypes.c_uint32)]
 
 
 SMALL_BATCH_DEFAULT = 32768     # include/at2v.h AT2V_SMALL_BATCH_DEFAULT
@@ -199,13 +200,15 @@ class BatchVerifier:
     """Owns an at2v context (one or more gfx950 devices)."""
 
     def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek", small_batch_max: int = 0,
-                 sender_cache: int = 0):
+                 sender_cache: int = 0, sender_comb: bool = False):
         """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
         0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel.
-        sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off)."""
+        sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off).
+        sender_comb: with sender_cache, also keep a comb of -A per cached key (660 KB each): chunks whose senders are
+        all cached verify by table additions only (at2v_comb.h), launches of every size."""
         self._lib = load_library()
         self.policy = _POLICIES[policy]
-        opts = _Opts(device, num_gpus, self.policy, small_batch_max, sender_cache)
+        opts = _Opts(device, num_gpus, self.policy, small_batch_max, sender_cache, 1 if sender_comb else 0)
         h = ctypes.c_void_p()
         _check(self._lib.at2v_create(ctypes.byref(opts), ctypes.byref(h)), "at2v_create")
         self._h = h

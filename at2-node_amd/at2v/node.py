@@ -65,6 +65,7 @@ class AccountError(Exception):
 
 
 QUEUE_EAGER = 1  # include/at2v.h AT2V_QUEUE_EAGER: also seal whenever no batch is in flight
+QUEUE_SENDER_COMB = 2  # include/at2v.h AT2V_QUEUE_SENDER_COMB: per-sender combs in the queue's context
 
 
 class _QueueOpts(ctypes.Structure):
@@ -141,11 +142,13 @@ class IngestQueue:
     """GPU-backed batching queue: submit records, poll (ticket, verdict) in submission order."""
 
     def __init__(self, device: int = 0, policy="dalek", max_batch: int = 65536, max_delay_us: int = 1000,
-                 max_msg_bytes: int = 256, depth: int = 3, eager: bool = False):
+                 max_msg_bytes: int = 256, depth: int = 3, eager: bool = False, sender_comb: bool = False):
+        """eager: also seal whenever no batch is in flight (latency mode); sender_comb: per-sender combs in the queue's
+        context (1024 keys; at2v_comb.h)"""
         from . import _POLICIES
         self._lib = _lib()
         o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth,
-                       QUEUE_EAGER if eager else 0)
+                       (QUEUE_EAGER if eager else 0) | (QUEUE_SENDER_COMB if sender_comb else 0))
         h = ctypes.c_void_p()
         _chk(self._lib.at2v_queue_create(ctypes.byref(o), ctypes.byref(h)), "at2v_queue_create")
         self._h = h

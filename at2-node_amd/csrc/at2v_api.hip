@@ -76,7 +76,7 @@ struct DevBuf {
 struct SenderCache {
   at2v::CacheArgs args{};
   hipEvent_t free = nullptr;  // recorded after every cached launch: cached launches never overlap (shared tags/slots)
-  DevBuf tags, entries, slot_of, new_list, ctl;
+  DevBuf tags, entries, slot_of, new_list, ctl, comb, bcomb;
   unsigned long long* host_ctl = nullptr;  // pinned copy of the device counters, refreshed after every cached launch
   hipEvent_t ctl_copied = nullptr;
   bool copy_pending = false;
@@ -165,6 +165,8 @@ void free_cache(SenderCache*& c) {
   c->entries.release();
   c->slot_of.release();
   c->new_list.release();
+  c->comb.release();
+  c->bcomb.release();
   c->ctl.release();
   if (c->host_ctl) (void)hipHostFree(c->host_ctl);
   if (c->ctl_copied) (void)hipEventDestroy(c->ctl_copied);
@@ -176,7 +178,7 @@ void free_cache(SenderCache*& c) {
 // Per-sender cache for `capacity` distinct keys on the current device: 2x as many tag slots (open addressing at
 // load <= 1/2), one entry per slot. AT2V_TEST_CACHE_FP_BITS (tests only) keeps that many fingerprint bits, so distinct
 // keys collide and the byte comparison in the verify kernel is exercised.
-int init_cache(Shard& s, uint32_t capacity, uint64_t seed) {
+int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
   SenderCache* c = new (std::nothrow) SenderCache;
   if (!c) return AT2V_E_OOM;
   s.cache = c;
@@ -195,7 +197,16 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed) {
   AT2V_TRY(c->entries.ensure((size_t)cap * at2v::cache_entry_bytes()));
   AT2V_TRY(c->ctl.ensure(ctl_bytes));
   AT2V_TRY(hipMemset(c->tags.p, 0, c->tags.cap));
+  AT2V_TRY(hipMemset(c->entries.p, 0, c->entries.cap));  // every entry invalid until a build kernel writes it
   AT2V_TRY(hipMemset(c->ctl.p, 0, c->ctl.cap));
+  if (comb) {  // one comb per key up to the capacity (claim index u -> comb u), and the comb of B
+    AT2V_TRY(c->comb.ensure((size_t)c->args.capacity * at2v::comb_bytes()));
+    AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes()));
+    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, s.stream));
+    AT2V_TRY(hipStreamSynchronize(s.stream));
+    c->args.comb = (int4*)c->comb.p;
+    c->args.bcomb = (const int4*)c->bcomb.p;
+  }
   AT2V_TRY(hipHostMalloc((void**)&c->host_ctl, c->ctl.cap, hipHostMallocDefault));
   std::memset(c->host_ctl, 0, c->ctl.cap);
   AT2V_TRY(hipEventCreateWithFlags(&c->ctl_copied, hipEventDisableTiming));
@@ -211,10 +222,10 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed) {
 // copy has landed), start over: clear the tags and the counters on the stream.
 hipError_t cache_before_launch(SenderCache& c, uint32_t n, hipStream_t stream) {
   hipError_t e = c.slot_of.ensure((size_t)n * 4);
-  if (e == hipSuccess) e = c.new_list.ensure((size_t)n * 8);
+  if (e == hipSuccess) e = c.new_list.ensure((size_t)n * 16);
   if (e != hipSuccess) return e;
   c.args.slot_of = (int*)c.slot_of.p;
-  c.args.new_list = (uint2*)c.new_list.p;
+  c.args.new_list = (uint4*)c.new_list.p;
   if (c.copy_pending && hipEventQuery(c.ctl_copied) == hipSuccess) {
     c.copy_pending = false;
     if (c.host_ctl[at2v::cache_ctl_full()]) {
@@ -237,8 +248,8 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   const int j = (int)(s.next_set++ % (unsigned)s.sets);
   hipError_t e = hipStreamWaitEvent(stream, s.scratch_free[j], 0);
   if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
-  // the cache serves the throughput kernel (launches above small_batch_max records)
-  SenderCache* c = (s.cache && n > ctx->pair_max) ? s.cache : nullptr;
+  // the cache serves the throughput kernel (launches above small_batch_max records; with combs, every launch)
+  SenderCache* c = (s.cache && (n > ctx->pair_max || s.cache->args.comb)) ? s.cache : nullptr;
   if (e == hipSuccess && c) e = hipStreamWaitEvent(stream, c->free, 0);
   if (e == hipSuccess && c) e = cache_before_launch(*c, n, stream);
   if (e == hipSuccess)
@@ -295,7 +306,7 @@ extern "C" {
 int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
-  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1, 0, 0};
+  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1, 0, 0, 0};
   if (opts) o = *opts;
   if (o.num_gpus <= 0) o.num_gpus = 1;
   if (o.policy != AT2V_POLICY_DALEK_V1 && o.policy != AT2V_POLICY_LIBSODIUM_1_0_18) return AT2V_E_INVALID;
@@ -314,7 +325,7 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   for (int g = 0; g < o.num_gpus; ++g) {
     int rc = init_shard(c->shards[(size_t)g], o.device + g);
     if (rc == AT2V_OK && o.sender_cache)
-      rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd());
+      rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd(), o.sender_comb != 0);
     if (rc != AT2V_OK) {
       (void)hipSetDevice(prev);
       at2v_destroy(c);
@@ -709,7 +720,8 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
     (void)hipGetDevice(&prev);
     if (hipSetDevice(sh.device) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
         hipMemcpy(w.data(), sh.cache->ctl.p, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      out->cache_entries += w[(size_t)at2v::cache_ctl_used()];
+      // claims since the last restart; those beyond the capacity are not built
+      out->cache_entries += std::min<uint64_t>(w[(size_t)at2v::cache_ctl_used()], sh.cache->args.capacity);
       out->cache_chunks += w[(size_t)at2v::cache_ctl_chunks()];
       out->cache_chunk_hits += w[(size_t)at2v::cache_ctl_chunk_hits()];
     }

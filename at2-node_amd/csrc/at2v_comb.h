@@ -1,0 +1,193 @@
+// at2v_comb.h — verify from per-key comb tables (at2v_opts.sender_comb).
+//
+// AT2 senders issue consecutive sequences (/root/reference/src/bin/server/accounts/account.rs:36-43): one public key A
+// signs many payloads. For such a key the device keeps a comb of -A, C[i][j] = [j 2^(8i)](-A) for i = 0..31, j = 0..128
+// (cached form), next to the context's comb of B, D[i][j] = [j 2^(16i)]B for i = 0..15, j = 0..2^15 (affine Niels).
+// Then dalek's point R' = [k](-A) + [s]B is a sum of 32 + 16 table entries, no doublings:
+//   k = sum_i e_i 2^(8i), e_i in [-128, 127] (sc_recode8)   ->  [k](-A) = sum_i +-C[i][|e_i|]
+//   s = sum_i f_i 2^(16i), f_i in [-2^15, 2^15) (sc_recode16) ->  [s]B   = sum_i +-D[i][|f_i|]
+// and the verdict is dalek's own comparison, enc(R') == R_bytes (the full-length form, DESIGN.md §4: no lattice
+// reduction, no decode of R). Any correct evaluation of [k](-A) + [s]B is the same group element, so the verdicts are
+// those of the ladder kernels (and of the oracle), for every key the comb was built from, small-order and mixed-order
+// keys included; a key that fails dalek's decode has verdict 0 whatever the comb holds.
+//
+// Cost per verify: 32 additions with cached entries (8 M) + 16 mixed additions (7 M) + one inversion (254 S + 11 M) +
+// SHA-512, against the half-size ladder's 2 exponentiations + 2 tables + 33 windows: ~3.5x fewer
+// multiplications. The comb of one key is 32 x 129 x 160 B = 660 KB, built once (comb_build_lane).
+//   TabC  : prefetch(stage, i, j) / load_prefetched(stage, gu_cached&)   entry C[i][j] of this lane's key
+//   TabBC : prefetch(stage, i, j) / load_prefetched(stage, gu_niels&)    entry D[i][j]
+// Two stages alternate: the entry of the next addition is fetched while this one is computed.
+#pragma once
+#include "at2v_gu.h"
+#include "at2v_verify.h"
+
+namespace at2v {
+
+constexpr int kCombPos = 32;          // A comb positions (radix 2^8)
+constexpr int kCombEntries = 129;     // j = 0..128 per position (j = 0: the identity)
+constexpr int kBCombPos = 16;         // B comb positions (radix 2^16)
+constexpr int kBCombEntries = 32769;  // j = 0..2^15
+constexpr int kCombGranules = 10;     // cached point: 40 words
+constexpr size_t kCombBytes = (size_t)kCombPos * kCombEntries * kCombGranules * 16;  // 660,480 B per key
+
+// R' (p2) encoded as dalek's CompressedEdwardsY (y canonical, sign bit = low bit of canonical x) == R_bytes
+AT2V_HD AT2V_INLINE int gu_encode_eq(const gu_p2& P, const uint32_t Rw[8]) {
+  fu zi, x, y;
+  fu_invert(zi, P.Z);
+  fu_mulc(x, P.X, zi);
+  fu_mulc(y, P.Y, zi);
+  uint32_t enc[8], xb[8];
+  fu_tobytes(enc, y);
+  fu_tobytes(xb, x);
+  enc[7] ^= (xb[0] & 1u) << 31;
+  int eq = 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= enc[i] == Rw[i];
+  return eq;
+}
+
+// dalek-1.x verify of one record from the comb of its key. a_ok: dalek's decode verdict for A (held with the comb).
+template <class TabC, class TabBC, class MsgWord>
+AT2V_HD AT2V_INLINE int verify_comb_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                       MsgWord msgword, int policy, int a_ok, const TabC& tc, const TabBC& tb) {
+  // V1: s < l; V2: A decodes (from the cache entry); libsodium's pre-rejects as in the ladder kernels
+  int ok = sc_is_canonical(Sw) & a_ok;
+  if (policy == POLICY_LIBSODIUM_1_0_18) {
+    ok &= !enc_small_order(Rw);
+    ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
+  }
+  // V3: k = SHA-512(R || A || M) mod l
+  uint32_t k[8];
+  {
+    uint32_t pre[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pre[i] = Rw[i];
+      pre[8 + i] = Aw[i];
+    }
+    uint64_t h[8];
+    sha512_msg<16>(h, pre, len, msgword);
+    uint32_t hw[16];
+    sha512_digest_words(hw, h);
+    sc_reduce512(k, hw);
+  }
+  AT2V_PHASE(5);
+  uint32_t kd[8], sd[8];
+  sc_recode8(kd, k);
+  sc_recode16(sd, Sw);
+  auto adig = [&](int i) -> int { return (int)((sel8(kd, i >> 2) >> (8 * (i & 3))) & 255) - 128; };
+  auto bdig = [&](int i) -> int { return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000; };
+  AT2V_PHASE(2);
+  // V4: R' = sum of the 32 A entries, then the 16 B entries; entry m + 1 is fetched while entry m is added
+  gu_p3 acc;
+  gu_p1p1 t;
+  gu_cached ca;
+  gu_niels nb;
+  gu_p3_identity(acc);
+  int e = adig(0);
+  tc.prefetch(0, 0, e < 0 ? -e : e);
+#pragma unroll 1
+  for (int i = 0; i < kCombPos; i += 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // stage h holds entry i + h
+      const int m = i + h;
+      const int en = m + 1 < kCombPos ? adig(m + 1) : bdig(0);
+      tc.load_prefetched(h, ca);
+      if (m + 1 < kCombPos)
+        tc.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
+      else
+        tb.prefetch(h ^ 1, 0, en < 0 ? -en : en);
+      gu_cached_cneg(ca, e < 0);
+      gu_add(t, acc, ca);
+      gu_p1p1_to_p3(acc, t);
+      e = en;
+    }
+  }
+#pragma unroll 1
+  for (int i = 0; i < kBCombPos; i += 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // the last A entry sat in stage 1, so B entry i + h is in stage h
+      const int m = i + h;
+      const int en = m + 1 < kBCombPos ? bdig(m + 1) : 0;
+      tb.load_prefetched(h, nb);
+      if (m + 1 < kBCombPos) tb.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
+      gu_niels_cneg(nb, e < 0);
+      gu_madd(t, acc, nb);
+      if (m + 1 < kBCombPos) gu_p1p1_to_p3(acc, t);
+      e = en;
+    }
+  }
+  AT2V_PHASE(4);
+  // V5/V6: dalek compares the compressed R' with the 32 bytes of R
+  gu_p2 Rp;
+  gu_p1p1_to_p2(Rp, t);
+  return ok & gu_encode_eq(Rp, Rw);
+}
+
+// One lane's share of the comb of key A: position pos (0..31), half h (0..1) -> entries j = 64h + 1 .. 64h + 64 of
+// C[pos][j] = [j 2^(8 pos)](-A), cached form, through store(j, const gu_cached&); the h = 0 lane also stores j = 0 (the
+// identity). 64 lanes (pos = lane >> 1, h = lane & 1) build the whole comb. Every lane decodes A (dalek rules) and
+// returns the decode verdict; an undecodable A yields a comb that no verdict depends on.
+template <class Store>
+AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, Store&& store) {
+  gu_p3 P;
+  const int ok = gu_frombytes(P, Aw);
+  fu_neg(P.X, P.X, FU_KC);  // -A
+  fu_carry(P.X);
+  fu_neg(P.T, P.T, FU_KC);
+  fu_carry(P.T);
+  // Pi = [2^(8 pos)](-A): every lane runs the 31 x 8 doublings and keeps its position's point
+  gu_p3 Pi = P, Q = P;
+  gu_p2 Q2;
+  gu_p1p1 t;
+#pragma unroll 1
+  for (int r = 1; r < kCombPos; ++r) {
+    gu_p3_to_p2(Q2, Q);
+#pragma unroll 1
+    for (int d = 0; d < 7; ++d) {
+      gu_p2_dbl(t, Q2);
+      gu_p1p1_to_p2(Q2, t);
+    }
+    gu_p2_dbl(t, Q2);
+    gu_p1p1_to_p3(Q, t);
+    if (r == pos) Pi = Q;
+  }
+  gu_cached c1;
+  gu_p3_to_cached(c1, Pi);
+  // first multiple of this half: [1]Pi (h = 0) or [65]Pi = [64]Pi + Pi (h = 1)
+  gu_p3 S = Pi;
+  {
+    gu_p2 D2;
+    gu_p3_to_p2(D2, Pi);
+#pragma unroll 1
+    for (int d = 0; d < 5; ++d) {
+      gu_p2_dbl(t, D2);
+      gu_p1p1_to_p2(D2, t);
+    }
+    gu_p2_dbl(t, D2);
+    gu_p3 D;
+    gu_p1p1_to_p3(D, t);
+    gu_add(t, D, c1);
+    gu_p3 S65;
+    gu_p1p1_to_p3(S65, t);
+    if (h) S = S65;
+  }
+  if (h == 0) {
+    gu_cached id;
+    gu_cached_identity(id);
+    store(0, id);
+  }
+  gu_cached cj;
+#pragma unroll 1
+  for (int m = 0; m < 64; ++m) {
+    gu_p3_to_cached(cj, S);
+    store(64 * h + 1 + m, cj);
+    if (m + 1 < 64) {
+      gu_add(t, S, c1);
+      gu_p1p1_to_p3(S, t);
+    }
+  }
+  return ok;
+}
+
+}  // namespace at2v

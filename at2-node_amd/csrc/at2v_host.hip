@@ -36,7 +36,11 @@ struct HipBackend {
   unsigned launches = 0;
 
   int init(const at2v_queue_opts& o) {
-    at2v_opts co{o.device, 1, o.policy};
+    at2v_opts co{o.device, 1, o.policy, 0, 0, 0};
+    if (o.flags & AT2V_QUEUE_SENDER_COMB) {
+      co.sender_cache = 1024;
+      co.sender_comb = 1;
+    }
     const int rc = at2v_create(&co, &ctx);
     if (rc) return rc;
     device = o.device;
@@ -158,7 +162,7 @@ int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (o.max_msg_bytes) qo.max_msg_bytes = o.max_msg_bytes;
   if (o.depth) qo.depth = (int)o.depth;
   qo.eager = (o.flags & AT2V_QUEUE_EAGER) != 0;
-  if (o.flags & ~AT2V_QUEUE_EAGER) return AT2V_E_INVALID;
+  if (o.flags & ~(AT2V_QUEUE_EAGER | AT2V_QUEUE_SENDER_COMB)) return AT2V_E_INVALID;
   if (qo.depth < 2 || qo.max_batch >= (1u << 31) || (uint64_t)qo.max_batch * qo.max_msg_bytes >= (1ull << 32))
     return AT2V_E_INVALID;
   at2v_queue* q = new (std::nothrow) at2v_queue;

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "at2v_cache.h"
+#include "at2v_comb.h"
 #include "at2v_verify.h"
 #include "at2v_verify_fu.h"
 #include "at2v_fe_fu.h"
@@ -237,6 +238,69 @@ struct DevTabB {
   }
 };
 
+// Comb entries (at2v_comb.h) by LDS-DMA into two alternating per-wave stages: the entry of the next addition lands while
+// this one is computed. TabC: C[i][j] of this lane's key (cached form, 10 granules); TabBC: D[i][j] (affine Niels, 8).
+struct DevComb {
+  const int4* base;  // this lane's key's comb
+  int4* stage[2];    // this wave's two 10 KiB stages (wave-uniform)
+  int lane;
+  __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's previous entry has been read out
+    const int4* src = base + ((size_t)i * kCombEntries + j) * kCombGranules;
+#pragma unroll
+    for (int q = 0; q < kCombGranules; ++q)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                       (__attribute__((address_space(3))) void*)(stage[st] + q * 64), 16, 0, 0);
+  }
+  template <class Cached>
+  __device__ AT2V_INLINE void load_prefetched(int st, Cached& c) const {
+    static_assert(sizeof(Cached) == 160, "cached point: 40 words");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t* w = reinterpret_cast<int32_t*>(&c);
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const int4 v = stage[st][q * 64 + lane];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+  }
+};
+struct DevBComb {
+  const int4* base;  // the context's comb of B
+  int4* stage[2];
+  int lane;
+  __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int4* src = base + ((size_t)i * kBCombEntries + j) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                       (__attribute__((address_space(3))) void*)(stage[st] + q * 64), 16, 0, 0);
+  }
+  template <class Niels>
+  __device__ AT2V_INLINE void load_prefetched(int st, Niels& n) const {
+    static_assert(sizeof(Niels) == 120, "Niels point: 30 words");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t w[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int4 v = stage[st][q * 64 + lane];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      n.ypx.v[k] = w[k];
+      n.ymx.v[k] = w[10 + k];
+      n.xy2d.v[k] = w[20 + k];
+    }
+  }
+};
+
 __device__ AT2V_INLINE void stage_btab(int4* lds) {
   const int4* src = reinterpret_cast<const int4*>(AT2V_BTAB);
   for (int i = threadIdx.x; i < AT2V_BTAB_ENTRIES * 8; i += blockDim.x) lds[i] = src[i];
@@ -325,21 +389,27 @@ struct Pace {
 #endif
 
 // ---- per-sender A cache (at2v_opts.sender_cache) ----
-// An entry: key = the 32 bytes of A (2 granules), meta = {dalek decode verdict of A, 0, 0, 0} (1 granule), then the
-// table [j]A, j = 0..8, in DevTabA's per-lane layout (90 granules). Tags: one 64-bit keyed fingerprint per entry (0 =
-// free), open addressing. A fingerprint only nominates an entry: the verify kernel takes it only after comparing all 32
-// key bytes with the record's A, so a collision costs speed, never a verdict.
+// An entry: key = the 32 bytes of A (2 granules), meta = {dalek decode verdict of A, valid, comb index, 0} (1 granule),
+// then the table [j]A, j = 0..8, in DevTabA's per-lane layout (90 granules; not built when the entry has a comb). Tags:
+// one 64-bit keyed fingerprint per entry (0 = free), open addressing. A fingerprint only nominates an entry: the verify
+// kernel takes it only if it is valid (built) and all 32 key bytes equal the record's A, so a collision or a claim
+// beyond the capacity costs speed, never a verdict. Entries are zeroed at creation (invalid); an entry is written only
+// by the build kernels, which run before the verify kernel of the same launch, and cached launches never overlap.
 constexpr int kCacheEntryGranules = 3 + kTabAGranules;
 enum : int { kCtlUsed = 0, kCtlFull, kCtlNew, kCtlFound, kCtlClaimed, kCtlFailed, kCtlChunkHits, kCtlChunks, kCtlWords };
 
-__device__ AT2V_INLINE bool cache_hit(const int4* __restrict__ cache, int slot, const uint32_t Aw[8], int& ok) {
+__device__ AT2V_INLINE bool cache_hit(const int4* __restrict__ cache, int slot, const uint32_t Aw[8], int& ok,
+                                      int& comb_idx) {
   ok = 0;
+  comb_idx = 0;
   if (slot < 0) return false;
   const int4* e = cache + (size_t)slot * kCacheEntryGranules;
   const int4 k0 = e[0], k1 = e[1], m = e[2];
   ok = m.x;
-  return (uint32_t)k0.x == Aw[0] && (uint32_t)k0.y == Aw[1] && (uint32_t)k0.z == Aw[2] && (uint32_t)k0.w == Aw[3] &&
-         (uint32_t)k1.x == Aw[4] && (uint32_t)k1.y == Aw[5] && (uint32_t)k1.z == Aw[6] && (uint32_t)k1.w == Aw[7];
+  comb_idx = m.z;
+  return m.y == 1 && (uint32_t)k0.x == Aw[0] && (uint32_t)k0.y == Aw[1] && (uint32_t)k0.z == Aw[2] &&
+         (uint32_t)k0.w == Aw[3] && (uint32_t)k1.x == Aw[4] && (uint32_t)k1.y == Aw[5] && (uint32_t)k1.z == Aw[6] &&
+         (uint32_t)k1.w == Aw[7];
 }
 
 // Half-size verification: one chunk of 64 records per wave, no final inversion. kCache: the per-sender A
@@ -347,13 +417,16 @@ __device__ AT2V_INLINE bool cache_hit(const int4* __restrict__ cache, int slot, 
 // cache_lookup_kernel + cache_build_kernel, launched just before on the same stream).
 // The body is a device function under two kernels with their own parameter lists, so the uncached kernel keeps exactly
 // round 2's signature and code (an extra-parameter template of it measured ~1% slower: profiles/r03b, r03d).
-template <bool kCache>
+// kComb (with kCache): entries carry per-key combs (at2v_comb.h); a wave whose 64 records all hit verifies from them
+// (additions only), any other wave runs the uncached half-size path.
+template <bool kCache, bool kComb = false>
 __device__ AT2V_INLINE void verify_chunks(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
     uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
     uint32_t* __restrict__ chunk_queue, const int* __restrict__ slot_of, const int4* __restrict__ cache,
-    unsigned long long* __restrict__ cache_ctl) {
+    unsigned long long* __restrict__ cache_ctl, const int4* __restrict__ comb = nullptr,
+    const int4* __restrict__ bcomb = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
@@ -447,17 +520,27 @@ __device__ AT2V_INLINE void verify_chunks(
 #if AT2V_FIELD_FU
     int good;
     if (kCache) {
-      int a_ok = 0;
-      const bool hit = cache_hit(cache, slot_of[ii], Aw, a_ok);
+      int a_ok = 0, comb_idx = 0;
+      const bool hit = cache_hit(cache, slot_of[ii], Aw, a_ok, comb_idx);
       const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
-      DevTabA tc{ta};
-      if (all_hit) tc.base = const_cast<int4*>(cache) + (size_t)slot_of[ii] * kCacheEntryGranules + 3;
       if (lane == 0) {
         atomicAdd(cache_ctl + kCtlChunks, 1ull);
         if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 1ull);
       }
-      good = verify_half_fu<true>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace, all_hit, a_ok) &
-             (i < n);
+      if (kComb) {
+        if (all_hit) {
+          const DevComb tc{comb + (size_t)comb_idx * (kCombBytes / 16), {astage + wib * 640, rstage + wib * 640}, lane};
+          const DevBComb tbc{bcomb, {astage + wib * 640, rstage + wib * 640}, lane};
+          good = verify_comb_fu(Rw, Aw, Sw, len, msgword, policy, a_ok, tc, tbc) & (i < n);
+        } else {
+          good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+        }
+      } else {
+        DevTabA tc{ta};
+        if (all_hit) tc.base = const_cast<int4*>(cache) + (size_t)slot_of[ii] * kCacheEntryGranules + 3;
+        good = verify_half_fu<true>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace, all_hit, a_ok) &
+               (i < n);
+      }
     } else {
       good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
     }
@@ -517,6 +600,19 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
                       slot_of, cache, cache_ctl);
+}
+
+// the same with per-key combs (at2v_opts.sender_comb): all-hit waves verify by additions only
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
+    const int* __restrict__ slot_of, const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl,
+    const int4* __restrict__ comb, const int4* __restrict__ bcomb) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  verify_chunks<true, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
+                            chunk_queue, slot_of, cache, cache_ctl, comb, bcomb);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -936,10 +1032,14 @@ __device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t 
 }
 
 // One lane per record: find A's entry by fingerprint (open addressing, 32 probes) or claim a free one (64-bit CAS).
-// slot_of[i] = entry or -1 (no room: the record takes the uncached path). Claims are reserved against the capacity per
-// wave (one atomic on the `used` counter for the wave's claimants, unused reservations given back), so the capacity
-// holds to within what concurrent waves have reserved but not yet returned. Claimed entries are listed for
-// cache_build_kernel; the statistics counters are aggregated per wave.
+// slot_of[i] = entry or -1 (no free slot on the probe path: the record takes the uncached path). Lanes of a wave that
+// want the same new key elect one leader, which claims for all of them. Claims are numbered after the fact (kCtlUsed,
+// since the last restart): a claim numbered below the capacity is built, one beyond it keeps its tag but stays invalid
+// (its records go uncached) and marks the cache full, so the host restarts it before a later launch. (A reservation
+// taken BEFORE claiming, round 3's first form, over-subscribed when many waves wanted the same keys at once: with
+// config-1 traffic every wave wants all 64 senders, 64 waves reserved 4096 > capacity, and the denied lanes re-probed
+// before the winning wave had claimed, so whole chunks missed.) Claimed entries are listed for the build kernels; the
+// statistics counters are aggregated per wave.
 __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -966,8 +1066,7 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
     }
   }
   // Lanes of this wave that want to claim the same key elect one leader (the lowest lane): AT2 traffic puts many records
-  // of one sender in a wave, and reserving once per record would exhaust the capacity with duplicates. One iteration
-  // per distinct wanted key in the wave.
+  // of one sender in a wave. One iteration per distinct wanted key in the wave.
   int leader = lane;
   {
     uint64_t pending = __ballot(want);
@@ -981,15 +1080,7 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
     }
   }
   const int follower = want && leader != lane;
-  want = want && !follower;
-  // reserve the wave's claims (one per distinct key) against the capacity
-  const uint64_t wm = __ballot(want);
-  unsigned long long base = 0;
-  if (lane == 0 && wm) base = atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(wm));
-  base = __shfl(base, 0);
-  const unsigned long long my = base + (unsigned long long)__popcll(wm & ((1ull << lane) - 1ull));
-  const int denied = want && my >= c.capacity;
-  if (want && !denied) {  // phase 2: claim along the probe path (a racing claimant may take the slot first)
+  if (want && !follower) {  // phase 2: claim along the probe path (a racing claimant may take the slot first)
     for (; k < 32; ++k) {
       const uint32_t j = (h + k) & mask;
       const unsigned long long old = atomicCAS(c.tags + j, 0ull, (unsigned long long)fp);
@@ -1012,25 +1103,13 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
       found = ls >= 0;
     }
   }
-  if (denied || (follower && slot < 0)) {  // phase 3: another wave may have claimed the key meanwhile (same probe path)
-    for (uint32_t q = 0; q < 32; ++q) {
-      const uint32_t j = (h + q) & mask;
-      const unsigned long long t = __hip_atomic_load(c.tags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == fp) {
-        slot = (int)j;
-        found = 1;
-        break;
-      }
-      if (t == 0) break;
-    }
-  }
   if (i < n) c.slot_of[i] = slot;
   const uint64_t cm = __ballot(claimed), fm = __ballot(found), xm = __ballot(i < n && slot < 0);
-  const uint64_t unused = wm & ~cm;  // reservations not turned into claims (denied, found, or no room)
-  unsigned long long nbase = 0;
+  unsigned long long nbase = 0, ubase = 0;
   if (lane == 0) {
-    if (unused) atomicAdd(c.ctl + kCtlUsed, (unsigned long long)-(long long)__popcll(unused));
     if (cm) {
+      ubase = atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(cm));
+      if (ubase + (unsigned long long)__popcll(cm) > c.capacity) atomicExch(c.ctl + kCtlFull, 1ull);
       nbase = atomicAdd(c.ctl + kCtlNew, (unsigned long long)__popcll(cm));
       atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
     }
@@ -1041,26 +1120,106 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
     }
   }
   nbase = __shfl(nbase, 0);
-  if (claimed) c.new_list[nbase + (unsigned long long)__popcll(cm & ((1ull << lane) - 1ull))] = make_uint2((uint32_t)slot, i);
+  ubase = __shfl(ubase, 0);
+  const unsigned long long rank = (unsigned long long)__popcll(cm & ((1ull << lane) - 1ull));
+  if (claimed) c.new_list[nbase + rank] = make_uint4((uint32_t)slot, i, (uint32_t)(ubase + rank), 0u);
 }
 
 // One lane per entry claimed by this launch: key, dalek decode verdict and [j]A (build_a_table, the verify kernel's own
-// steps). Threads beyond the launch's claim count leave at once.
+// steps), or, with combs on, the key and verdict only (cache_comb_kernel builds the comb). A claim beyond the capacity
+// is written invalid. Threads beyond the launch's claim count leave at once.
 __global__ __launch_bounds__(256) void cache_build_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   if ((unsigned long long)t >= __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const uint2 e = c.new_list[t];
+  const uint4 e = c.new_list[t];
+  int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
+  if (e.z >= c.capacity) {
+    ent[2] = make_int4(0, 0, 0, 0);  // invalid: the tag stays (its key keeps finding this slot) until the restart
+    return;
+  }
   uint32_t a[8];
   load8(a, pk + (size_t)e.y * 32);
-  int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
-  DevTabA tw{ent + 3, nullptr, 0, nullptr};  // store() only
-  const int ok = build_a_table(a, tw);
+  int ok;
+  if (c.comb) {
+    gu_p3 A;
+    ok = gu_frombytes(A, a);
+  } else {
+    DevTabA tw{ent + 3, nullptr, 0, nullptr};  // store() only
+    ok = build_a_table(a, tw);
+  }
   ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
   ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
-  ent[2] = make_int4(ok, 0, 0, 0);
+  ent[2] = make_int4(ok, 1, (int)e.z, 0);
+}
+
+// One wave per entry claimed (and built) by this launch: the comb of -A at claim index u (comb_build_lane, lane =
+// position x half). Persistent grid over the launch's claims.
+__global__ __launch_bounds__(256) void cache_comb_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * 4;
+  const unsigned long long cnt = __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < cnt; t += nw) {
+    const uint4 e = c.new_list[t];
+    if (e.z >= c.capacity) continue;  // wave-uniform
+    uint32_t a[8];
+    load8(a, pk + (size_t)e.y * 32);
+    int4* cb = c.comb + (size_t)e.z * (kCombBytes / 16);
+    const int pos = lane >> 1;
+    comb_build_lane(a, pos, lane & 1, [&](int j, const gu_cached& p) {
+      const int32_t* w = reinterpret_cast<const int32_t*>(&p);
+      int4* dst = cb + ((size_t)pos * kCombEntries + j) * kCombGranules;
+#pragma unroll
+      for (int q = 0; q < kCombGranules; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    });
+  }
+}
+
+// D[pos][j] = [j 2^(16 pos)]B, j = 0..2^15, affine Niels on the unsigned field: one lane per entry, (j 2^(16 pos)) mod l
+// through the signed-field base ladder (as build_btab_kernel), built once per context with combs on.
+__global__ __launch_bounds__(kBlock) void build_bcomb_kernel(int4* __restrict__ out, int pos) {
+  __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
+  stage_btab(btab);
+  LdsTabB tb{btab};
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (uint32_t)kBCombEntries) return;
+  uint32_t x[16], k[8];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) x[q] = 0;
+  const int bit = 16 * pos;
+  x[bit >> 5] = j << (bit & 31);  // j <= 2^15: the halfword at bit 16 pos fits its word
+  sc_reduce512(k, x);
+  ge_p2 P;
+  ge_scalarmult_base(P, k, tb);
+  ge_niels nj;
+  ge_p2_to_niels(nj, P);
+  gu_niels nu;
+  niels_fe_to_fu(nu, nj);
+  int32_t w[32];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) {
+    w[q] = (int32_t)nu.ypx.v[q];
+    w[10 + q] = (int32_t)nu.ymx.v[q];
+    w[20 + q] = (int32_t)nu.xy2d.v[q];
+  }
+  w[30] = w[31] = 0;
+  int4* dst = out + ((size_t)pos * kBCombEntries + j) * 8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
 size_t cache_entry_bytes() { return (size_t)kCacheEntryGranules * 16; }
+size_t comb_bytes() { return kCombBytes; }
+size_t bcomb_bytes() { return (size_t)kBCombPos * kBCombEntries * 8 * 16; }
+
+hipError_t launch_build_bcomb(int4* out, hipStream_t stream) {
+  for (int pos = 0; pos < kBCombPos; ++pos) {
+    hipLaunchKernelGGL(build_bcomb_kernel, dim3((kBCombEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out,
+                       pos);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
 int cache_ctl_words() { return kCtlWords; }
 int cache_ctl_used() { return kCtlUsed; }
 int cache_ctl_full() { return kCtlFull; }
@@ -1075,6 +1234,12 @@ hipError_t launch_cache_prepare(const CacheArgs& c, const uint8_t* pk, uint32_t 
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(cache_build_kernel, dim3(blocks), dim3(256), 0, stream, pk, c);
+  e = hipGetLastError();
+  if (e != hipSuccess || !c.comb) return e;
+  // one wave per claim; claims of a launch <= its records, and <= the capacity get built
+  const uint32_t waves = n < c.capacity ? n : c.capacity;
+  const uint32_t cblocks = ((waves < 2048u ? waves : 2048u) + 3) / 4;
+  hipLaunchKernelGGL(cache_comb_kernel, dim3(cblocks), dim3(256), 0, stream, pk, c);
   return hipGetLastError();
 }
 
@@ -1104,7 +1269,7 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
                          const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache) {
   if (n == 0) return hipSuccess;
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
-  if (n <= pair_max) {
+  if (n <= pair_max && !(cache && cache->comb)) {  // (with combs, small batches take the comb kernel: faster still)
     // one wave (32 records) per SIMD: 4-wave blocks; the context's scratch holds grid x 8 waves of (larger) slots
     const uint32_t nchunks = (n + 31) / 32;
     const uint32_t cap_blocks = (uint32_t)grid * kWavesPerBlock / kPairWaves;
@@ -1126,6 +1291,12 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   if (cache) {
     const hipError_t ce = launch_cache_prepare(*cache, pk, n, stream);
     if (ce != hipSuccess) return ce;
+    if (cache->comb) {
+      hipLaunchKernelGGL(verify_kernel_comb, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+                         verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl,
+                         (const int4*)cache->comb, cache->bcomb);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL(verify_kernel_cached, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
                        verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl);
     return hipGetLastError();

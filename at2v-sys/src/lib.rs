@@ -31,7 +31,7 @@ pub struct At2vLedger {
 
 /// include/at2v.h AT2V_ABI_VERSION: the layouts of the #[repr(C)] structs below. `BatchVerifier::new` and
 /// `Queue::new` refuse a library that reports another version (the structs are copied whole by the library).
-pub const AT2V_ABI_VERSION: c_int = 3;
+pub const AT2V_ABI_VERSION: c_int = 4;
 
 pub const AT2V_POLICY_DALEK_V1: c_int = 0;
 pub const AT2V_POLICY_LIBSODIUM_1_0_18: c_int = 1;
@@ -78,6 +78,8 @@ pub struct At2vOpts {
     pub small_batch_max: u32,
     /// per-sender A cache capacity in distinct public keys; 0 = off
     pub sender_cache: u32,
+    /// with sender_cache: 1 = per-key combs (all-hit chunks verify by table additions only); 0 = off
+    pub sender_comb: u32,
 }
 
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
@@ -115,6 +117,7 @@ pub struct At2vQueueOpts {
 
 /// `At2vQueueOpts::flags`: also seal the filling batch whenever no batch is in flight (latency mode).
 pub const AT2V_QUEUE_EAGER: u32 = 1;
+pub const AT2V_QUEUE_SENDER_COMB: u32 = 2;
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]

@@ -53,6 +53,8 @@ def parse():
                     help="0 = distinct keys (BASELINE config 2); K > 0 = record i signed by sender i %% K (AT2 traffic)")
     ap.add_argument("--sender-cache", type=int, default=0,
                     help="at2v_opts.sender_cache: per-sender A cache capacity in keys (0 = off)")
+    ap.add_argument("--sender-comb", type=int, default=0,
+                    help="at2v_opts.sender_comb: 1 = per-key combs with the cache (all-hit chunks by table additions)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="max records for the CPU baseline sample (0 = skip); sized to ~3 s on the threads used")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
@@ -190,7 +192,8 @@ def main():
 
     n, L = args.records_per_gpu, args.msg_len
     n = (n + 63) // 64 * 64
-    v = at2v.BatchVerifier(device=local, policy=args.policy, sender_cache=args.sender_cache)
+    v = at2v.BatchVerifier(device=local, policy=args.policy, sender_cache=args.sender_cache,
+                           sender_comb=bool(args.sender_comb))
     if use_dist:
         uid = [at2v.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -286,7 +289,8 @@ def main():
             workload = "BASELINE config 3: 16M signatures index-sharded over 8 MI355X + RCCL all-gather of the verdict bitmap"
         elif args.senders:
             workload = (f"{n} signed transfers per GPU ({L}-byte M) from {args.senders} repeating senders (AT2 traffic)"
-                        + (f", per-sender A cache of {args.sender_cache} keys" if args.sender_cache else ", no cache"))
+                        + (f", per-sender A cache of {args.sender_cache} keys" if args.sender_cache else ", no cache")
+                        + (" with per-key combs" if args.sender_cache and args.sender_comb else ""))
         elif n == 1 << 20:
             workload = (f"BASELINE config 2: 1M signed transfers per GPU (100-byte M), dalek-1.x verify"
                         + (f"; {world} GPUs, weak scaling, RCCL all-gather of the verdict bitmap" if world > 1 else ""))
@@ -312,6 +316,7 @@ def main():
                 "policy": args.policy,
                 "senders": args.senders or "distinct",
                 "sender_cache": args.sender_cache,
+                "sender_comb": bool(args.sender_cache and args.sender_comb),
                 "parallelism": f"index-shard x{world}" + (" + RCCL all-gather of verdict words (libat2v)" if use_dist else ""),
             },
             "verdict_match": match,
@@ -477,7 +482,8 @@ def _pmc_pass(args, n, L, counters):
     cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", *counters, "--kernel-trace", "--output-format", "csv",
            "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "0",
            "--cpu-sample", "0", "--pmc-traffic", "0", "--records-per-gpu", str(n), "--msg-len", str(L),
-           "--policy", args.policy, "--senders", str(args.senders), "--sender-cache", str(args.sender_cache), "--e2e", "0"]
+           "--policy", args.policy, "--senders", str(args.senders), "--sender-cache", str(args.sender_cache),
+           "--sender-comb", str(args.sender_comb), "--e2e", "0"]
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150, check=True)
         rows, durs = [], []

@@ -26,10 +26,11 @@ extern "C" {
 #endif
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
- * version 3 appended at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
+ * version 4 appended at2v_opts.sender_comb and the AT2V_QUEUE_SENDER_COMB queue flag; version 3 appended
+ * at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
  * at2v_opts.small_batch_max and at2v_queue_opts.flags). A binding checks at2v_abi_version() == AT2V_ABI_VERSION
  * before passing any struct (the Python and Rust bindings in this repo refuse a mismatching library). */
-#define AT2V_ABI_VERSION 3
+#define AT2V_ABI_VERSION 4
 int at2v_abi_version(void);
 
 typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, and the RCCL
@@ -50,6 +51,11 @@ typedef struct {
                                public keys, 0 = off. When full it is cleared and refilled. A record whose sender A is cached skips decoding A and building
                                its [j]A table; the verdict is unchanged (the cache holds only values derived from the
                                32 bytes of A, and every hit is confirmed by comparing those bytes). */
+  uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(8i)](-A), 660 KB
+                               per key, sender_cache x 660 KB per device, plus a 67 MB comb of B per context), and a
+                               64-record chunk whose senders are all cached is verified by 48 table additions and one
+                               inversion instead of the doubling ladder (~3x fewer multiplications; launches of any size,
+                               small batches included). Same verdicts. 0 = off. */
 } at2v_opts;
 #define AT2V_SMALL_BATCH_DEFAULT 32768u
 #define AT2V_SMALL_BATCH_OFF 0xffffffffu
@@ -197,9 +203,11 @@ typedef struct {
   uint32_t max_delay_us;  /* deadline of the oldest pending record; 0 = 1000 */
   uint32_t max_msg_bytes; /* message bytes budgeted per record (slot capacity max_batch x this); 0 = 256 */
   uint32_t depth;         /* batch slots, >= 2; 0 = 3 */
-  uint32_t flags;         /* AT2V_QUEUE_EAGER: also seal whenever no batch is in flight */
+  uint32_t flags;         /* AT2V_QUEUE_EAGER: also seal whenever no batch is in flight; AT2V_QUEUE_SENDER_COMB:
+                             per-sender combs (at2v_opts.sender_comb) */
 } at2v_queue_opts;
 #define AT2V_QUEUE_EAGER 1u
+#define AT2V_QUEUE_SENDER_COMB 2u /* the queue's context gets sender_cache = 1024 keys with sender_comb = 1 */
 typedef struct {
   uint64_t submitted, completed, batches, failed_batches;
   double mean_batch;           /* records per completed batch */

@@ -6,6 +6,9 @@
 #include <cstring>
 #include <vector>
 
+#include <map>
+
+#include "at2v_comb.h"
 #include "at2v_verify.h"
 #include "at2v_verify_fu.h"
 #include "at2v_fe_fu.h"
@@ -102,6 +105,48 @@ struct HostTabBFu {
   void load_prefetched(gu_niels& n) const { n = t[pending]; }
 };
 
+// comb of one key (at2v_comb.h), built by the 64 lanes' comb_build_lane exactly as the device's builder does
+struct HostComb {
+  std::vector<gu_cached> e;
+  int a_ok = 0;
+  mutable int pend[2] = {0, 0};
+  explicit HostComb(const uint32_t A[8]) : e((size_t)kCombPos * kCombEntries) {
+    for (int lane = 0; lane < 64; ++lane) {
+      const int pos = lane >> 1;
+      a_ok = comb_build_lane(A, pos, lane & 1,
+                             [&](int j, const gu_cached& c) { e[(size_t)pos * kCombEntries + j] = c; });
+    }
+  }
+  void prefetch(int st, int i, int j) const { pend[st] = i * kCombEntries + j; }
+  void load_prefetched(int st, gu_cached& c) const { c = e[pend[st]]; }
+};
+// D[i][j] = [j 2^(16 i)]B on demand: (j 2^(16 i)) mod l times B by the signed-field base ladder, then the unsigned form
+struct HostBComb {
+  mutable std::map<uint64_t, gu_niels> t;
+  mutable uint64_t pend[2] = {0, 0};
+  void prefetch(int st, int i, int j) const { pend[st] = ((uint64_t)i << 32) | (uint32_t)j; }
+  void load_prefetched(int st, gu_niels& n) const {
+    auto it = t.find(pend[st]);
+    if (it == t.end()) {
+      const int i = (int)(pend[st] >> 32);
+      const uint32_t j = (uint32_t)pend[st];
+      uint32_t x[16] = {0}, k[8];
+      const int bit = 16 * i;
+      x[bit >> 5] |= j << (bit & 31);
+      if ((bit & 31) && (bit >> 5) + 1 < 16) x[(bit >> 5) + 1] |= (uint32_t)((uint64_t)j >> (32 - (bit & 31)));
+      sc_reduce512(k, x);
+      ge_p2 P;
+      ge_scalarmult_base(P, k, HostTabB8());
+      ge_niels ns;
+      ge_p2_to_niels(ns, P);
+      gu_niels nu;
+      niels_fe_to_fu(nu, ns);
+      it = t.emplace(pend[st], nu).first;
+    }
+    n = it->second;
+  }
+};
+
 static void words(uint32_t w[8], const uint8_t* b) {
   for (int i = 0; i < 8; ++i) w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
@@ -120,8 +165,11 @@ int main(int argc, char** argv) {
   (void)ok;
   size_t bad_d = 0, bad_s = 0;
   int limit = argc > 2 ? atoi(argv[2]) : (int)n;
-  // 1: the half-size equation (verify_half); 2: on the unsigned field; 3: two lanes per signature (verify_pair_part)
+  // 1: the half-size equation (verify_half); 2: on the unsigned field; 3: two lanes per signature (verify_pair_part);
+  // 4: from per-key combs (verify_comb_fu, the sender-comb path)
   const int half = argc > 3 ? atoi(argv[3]) : 0;
+  std::map<std::vector<uint32_t>, HostComb*> combs;
+  HostBComb bcomb;
   for (size_t i = 0; i < n && (int)i < limit; ++i) {
     uint32_t R[8], A[8], S[8];
     words(R, &sig[64 * i]);
@@ -137,7 +185,14 @@ int main(int argc, char** argv) {
     static HostTabB16 tb;
     HostTabA ta, tr;
     int d, s;
-    if (half == 3) {
+    if (half == 4) {
+      std::vector<uint32_t> key(A, A + 8);
+      auto it = combs.find(key);
+      if (it == combs.end()) it = combs.emplace(key, new HostComb(A)).first;
+      const HostComb& c = *it->second;
+      d = verify_comb_fu(R, A, S, len, mw, POLICY_DALEK_V1, c.a_ok, c, bcomb);
+      s = verify_comb_fu(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, c.a_ok, c, bcomb);
+    } else if (half == 3) {
       static HostTabB16Hi tb1s;
       static HostTabBFu<HostTabB16> fb0(tb);
       static HostTabBFu<HostTabB16Hi> fb1(tb1s);

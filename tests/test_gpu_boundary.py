@@ -174,3 +174,23 @@ def test_config5_mininode_eager_latency(at2v_mod):
     assert all(p["failed"] == 0 and p["rejected"] == r["bad_signatures"] for p in r["per_node"])
     p50 = [p["queue_p50_us"] for p in r["per_node"]]
     assert max(p50) <= 1000.0, f"queue p50 per node {p50} us > 1.0 ms"
+
+
+@pytest.mark.timeout(600)
+def test_config5_mininode_comb_latency(at2v_mod):
+    """BASELINE config 5 in latency mode with per-sender combs in every node's queue (AT2V_QUEUE_SENDER_COMB): the 64
+    client keys get combs on first sight, then every small batch verifies by table additions (at2v_comb.h). Same
+    correctness bar as above; latency gate: every node's queue submit->verdict p50 <= 0.4 ms. The
+    measured latency goes to gpurun_out/config5_comb.json."""
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mininode.py"), "--nodes", "4", "--rate", "20000",
+                          "--seconds", "2", "--batch", "1024", "--delay-us", "1000", "--eager", "1", "--comb", "1"],
+                         capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    with open(os.path.join(ROOT, "gpurun_out", "config5_comb.json"), "w") as fp:
+        json.dump(r, fp, indent=1)
+    assert r["ledgers_identical"] and r["all_real_applied"] and r["bad_signatures"] > 0
+    assert all(p["failed"] == 0 and p["rejected"] == r["bad_signatures"] for p in r["per_node"])
+    p50 = [p["queue_p50_us"] for p in r["per_node"]]
+    assert max(p50) <= 400.0, f"queue p50 per node {p50} us > 0.4 ms"

@@ -6,7 +6,8 @@ payloads of a node batch (client.rs:77-78). With the cache on, a wave whose 64 r
 must stay a pure function of (A, R||S, M): every test here compares with the oracle or the golden fixtures, through
 the C ABI, in every cache state — entry built in the same launch, warm, fingerprint collisions (forced with
 AT2V_TEST_CACHE_FP_BITS), cache full (restart), undecodable / small-order / non-canonical senders cached together with
-their decode verdict, and both policies."""
+their decode verdict, and both policies. Every test runs twice: with the [j]A tables (sender_comb off) and with per-key
+combs (sender_comb on: all-hit chunks verify by table additions only, at2v_comb.h)."""
 import os
 
 import numpy as np
@@ -18,6 +19,11 @@ pytestmark = pytest.mark.gpu
 
 CFG_SEED = 0x4154325F
 OFF = 0xFFFFFFFF  # small_batch_max: the cache serves the throughput kernel, so run it at every size
+
+
+@pytest.fixture(params=[False, True], ids=["tables", "comb"])
+def comb(request):
+    return request.param
 
 
 @pytest.fixture(scope="module")
@@ -44,7 +50,7 @@ def _mutate(pk, sig, msg, off, rng, k):
     return pk, sig, msg
 
 
-def test_config1_traffic_every_chunk_hits(at2v_mod, oracle):
+def test_config1_traffic_every_chunk_hits(at2v_mod, oracle, comb):
     """BASELINE config 1 traffic (64 senders x sequences 1..64): every entry is built by the first launch's build pass,
     so every chunk of every launch takes the cached path; verdicts equal the oracle's, mutated records included."""
     pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
@@ -53,7 +59,7 @@ def test_config1_traffic_every_chunk_hits(at2v_mod, oracle):
     want = oracle.verify_batch(pk, sig, msg, off)
     want2 = oracle.verify_batch(pk2, sig2, msg2, off)
     assert want.all() and 0 < want2.sum() < len(want2)
-    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024) as v:
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=comb) as v:
         for rep in range(2):
             assert np.array_equal(v.verify_batch(pk, sig, msg, off), want)
         info = v.info()
@@ -65,10 +71,10 @@ def test_config1_traffic_every_chunk_hits(at2v_mod, oracle):
 
 
 @pytest.mark.parametrize("policy", ["dalek", "libsodium"])
-def test_golden_sets_with_cache(at2v_mod, golden, policy):
+def test_golden_sets_with_cache(at2v_mod, golden, policy, comb):
     """every golden fixture set, twice (cold, then warm cache), both policies: the small-order, non-canonical and
     off-curve senders of the adversarial/edge sets are cached with their decode verdicts"""
-    with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 15) as v:
+    with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 15, sender_comb=comb) as v:
         for name in golden_io.SETS:
             g = golden[name]
             want = g.dalek if policy == "dalek" else g.sodium
@@ -77,7 +83,7 @@ def test_golden_sets_with_cache(at2v_mod, golden, policy):
                 assert np.array_equal(got, want), (name, rep, np.nonzero(got != want)[0][:10])
 
 
-def test_repeated_adversarial_senders(at2v_mod, oracle):
+def test_repeated_adversarial_senders(at2v_mod, oracle, comb):
     """an adversarial batch whose senders repeat: 512 distinct records (every class of config 4) tiled 32x with fresh
     mutations, so entries for small-order / undecodable keys are hit by many records"""
     pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 21, 0, 512, 100)
@@ -88,33 +94,33 @@ def test_repeated_adversarial_senders(at2v_mod, oracle):
     off_t = (np.arange(512 * 32 + 1) * L).astype(np.uint32)
     pk_t, sig_t, msg_t = _mutate(pk_t, sig_t, msg_t, off_t, np.random.default_rng(5), 1500)
     want = oracle.verify_batch(pk_t, sig_t, msg_t, off_t)
-    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=4096) as v:
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=4096, sender_comb=comb) as v:
         for rep in range(2):
             got = v.verify_batch(pk_t, sig_t, msg_t, off_t)
             assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
 
 
-def test_fingerprint_collisions_fall_back(at2v_mod, oracle, monkeypatch):
+def test_fingerprint_collisions_fall_back(at2v_mod, oracle, monkeypatch, comb):
     """3 fingerprint bits (test hook): distinct senders share fingerprints, so the lookup nominates entries of other
     keys; the byte comparison must send those waves down the uncached path with identical verdicts"""
     monkeypatch.setenv("AT2V_TEST_CACHE_FP_BITS", "3")
     pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
     pk2, sig2, msg2 = _mutate(pk, sig, msg, off, np.random.default_rng(7), 200)
     want = oracle.verify_batch(pk2, sig2, msg2, off)
-    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024) as v:
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=comb) as v:
         for rep in range(2):
             assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want)
         info = v.info()
         assert info["cache_entries"] <= 4 and info["cache_chunk_hits"] < info["cache_chunks"]
 
 
-def test_cache_full_restarts(at2v_mod, oracle):
+def test_cache_full_restarts(at2v_mod, oracle, comb):
     """capacity 16 < 64 senders: the first launch fills the cache (the rest go uncached), a later launch starts over;
-    verdicts exact throughout. Claims are reserved against the capacity per wave, so it holds exactly."""
+    verdicts exact throughout. Claims beyond the capacity keep their tags but are never built (invalid entries)."""
     pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
     pk2, sig2, msg2 = _mutate(pk, sig, msg, off, np.random.default_rng(9), 100)
     want = oracle.verify_batch(pk2, sig2, msg2, off)
-    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=16) as v:
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=16, sender_comb=comb) as v:
         for rep in range(4):
             assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want), rep
             assert v.info()["cache_entries"] <= 16
@@ -150,3 +156,24 @@ def test_generator_with_repeating_senders(at2v_mod, oracle):
                              torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
     assert (d2.cpu().numpy().reshape(S, 32) == pk[:S]).all()
+
+
+@pytest.mark.parametrize("n", [1, 20, 64, 100, 2048, 40_000])
+def test_comb_small_and_ragged_launches(at2v_mod, oracle, n):
+    """with combs on, launches of every size take the comb kernel (the low-latency pair kernel is not used): config-1
+    traffic cut to n records, mutated, cold then warm, against the oracle"""
+    pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
+    reps = (n + len(pk) - 1) // len(pk)
+    L = 48
+    pk = np.tile(pk, (reps, 1))[:n]
+    sig = np.tile(sig, (reps, 1))[:n]
+    msg = np.tile(msg, reps)[: n * L]
+    off = (np.arange(n + 1) * L).astype(np.uint32)
+    pk, sig, msg = _mutate(pk, sig, msg, off, np.random.default_rng(n), max(1, n // 10))
+    want = oracle.verify_batch(pk, sig, msg, off)
+    with at2v_mod.BatchVerifier(sender_cache=1024, sender_comb=True) as v:
+        for rep in range(2):
+            got = v.verify_batch(pk, sig, msg, off)
+            assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
+        info = v.info()
+        assert info["cache_chunk_hits"] > 0

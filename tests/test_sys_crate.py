@@ -238,8 +238,10 @@ def test_integration_md_struct_definitions_match_header():
 
 def test_safe_layer_checks_abi_version():
     src = open(os.path.join(CRATE, "src", "lib.rs")).read()
-    assert "pub const AT2V_ABI_VERSION: c_int = 3;" in src
-    assert re.search(r"#define AT2V_ABI_VERSION 3\b", open(HEADER).read())
+    v = re.search(r"#define AT2V_ABI_VERSION (\d+)\b", open(HEADER).read()).group(1)
+    assert f"pub const AT2V_ABI_VERSION: c_int = {v};" in src
+    import at2v
+    assert int(v) == at2v.ABI_VERSION
     for ctor in ("impl BatchVerifier", "impl Queue"):
         body = src[src.index(ctor):]
         body = body[:body.index("\n}\n")]

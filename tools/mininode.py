@@ -37,7 +37,7 @@ def node_main(idx, inboxes, result_q, args, total):
     from at2v.node import VERDICT_FAILED, IngestQueue, Ledger, SendAssetRequest, pack_send_asset, verdict_mask
 
     q = IngestQueue(device=0, max_batch=args.batch, max_delay_us=args.delay_us, max_msg_bytes=48, depth=3,
-                    eager=args.eager)
+                    eager=args.eager, sender_comb=bool(args.comb))
     led = Ledger()
     lock = threading.Lock()
     chunks = []  # submitted runs, ticket order: [first, pk, seq, rcp, amt, t_arrival]
@@ -212,6 +212,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="queue flush size B")
     ap.add_argument("--delay-us", type=int, default=1000, help="queue flush deadline Δ")
     ap.add_argument("--eager", type=int, default=0, help="1 = queue latency mode: also seal whenever no batch is in flight")
+    ap.add_argument("--comb", type=int, default=0, help="1 = per-sender combs in each node's queue context (at2v_comb.h)")
     ap.add_argument("--senders", type=int, default=64)
     ap.add_argument("--bad-frac", type=float, default=0.02)
     ap.add_argument("--max-amount", type=int, default=10,
