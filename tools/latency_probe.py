@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--sizes", default="1,20,64,1024")
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--msg-len", type=int, default=48)
+    ap.add_argument("--comb", type=int, default=0, help="1 = per-sender combs (the keys are cached after the first rep)")
     a = ap.parse_args()
     import torch
 
@@ -42,9 +43,9 @@ def main():
     sizes = [int(x) for x in a.sizes.split(",")]
     nmax = max(sizes)
     pk, sig, msg, off = o.gen_records(0x4154325F, 0, nmax, a.msg_len)
-    out = {"msg_len": a.msg_len, "reps": a.reps, "sizes": {}}
-    v = at2v.BatchVerifier(device=0)
-    q = IngestQueue(device=0, max_batch=4096, max_delay_us=1000, eager=True)
+    out = {"msg_len": a.msg_len, "reps": a.reps, "comb": bool(a.comb), "sizes": {}}
+    v = at2v.BatchVerifier(device=0, sender_cache=1024 if a.comb else 0, sender_comb=bool(a.comb))
+    q = IngestQueue(device=0, max_batch=4096, max_delay_us=1000, eager=True, sender_comb=bool(a.comb))
     s = torch.cuda.current_stream()
     for B in sizes:
         p, g, m, f = pk[:B], sig[:B], msg[:f_end(off, B)], off[:B + 1]
