@@ -16,7 +16,9 @@
 // multiplications. The comb of one key is 32 x 129 x 160 B = 660 KB, built once (comb_build_lane).
 //   TabC  : prefetch(stage, i, j) / load_prefetched(stage, gu_cached&)   entry C[i][j] of this lane's key
 //   TabBC : prefetch(stage, i, j) / load_prefetched(stage, gu_niels&)    entry D[i][j]
-// Two stages alternate: the entry of the next addition is fetched while this one is computed.
+// Two stages alternate: the entry of the next addition is fetched while this one is computed. The low-latency kernel
+// splits one record's work over four waves (decode R | 16 B entries | SHA-512 + 16 A entries | SHA-512 + 16 A entries)
+// and compares R' with the decoded R projectively (comb_check_split).
 #pragma once
 #include "at2v_gu.h"
 #include "at2v_verify.h"
@@ -46,82 +48,129 @@ AT2V_HD AT2V_INLINE int gu_encode_eq(const gu_p2& P, const uint32_t Rw[8]) {
   return eq;
 }
 
-// dalek-1.x verify of one record from the comb of its key. a_ok: dalek's decode verdict for A (held with the comb).
-template <class TabC, class TabBC, class MsgWord>
-AT2V_HD AT2V_INLINE int verify_comb_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
-                                       MsgWord msgword, int policy, int a_ok, const TabC& tc, const TabBC& tb) {
-  // V1: s < l; V2: A decodes (from the cache entry); libsodium's pre-rejects as in the ladder kernels
+// Checks that need no point arithmetic: V1 (s < l), A's decode verdict (held with the comb), libsodium's pre-rejects.
+AT2V_HD AT2V_INLINE int comb_prechecks(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], int policy,
+                                       int a_ok) {
   int ok = sc_is_canonical(Sw) & a_ok;
   if (policy == POLICY_LIBSODIUM_1_0_18) {
     ok &= !enc_small_order(Rw);
     ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
   }
-  // V3: k = SHA-512(R || A || M) mod l
+  return ok;
+}
+
+// V3 and the recoding of k: kd = signed radix-256 digits of SHA-512(R || A || M) mod l
+template <class MsgWord>
+AT2V_HD AT2V_INLINE void comb_k_digits(uint32_t kd[8], const uint32_t Rw[8], const uint32_t Aw[8], uint32_t len,
+                                       MsgWord msgword) {
   uint32_t k[8];
-  {
-    uint32_t pre[16];
+  uint32_t pre[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      pre[i] = Rw[i];
-      pre[8 + i] = Aw[i];
-    }
-    uint64_t h[8];
-    sha512_msg<16>(h, pre, len, msgword);
-    uint32_t hw[16];
-    sha512_digest_words(hw, h);
-    sc_reduce512(k, hw);
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = Rw[i];
+    pre[8 + i] = Aw[i];
   }
-  AT2V_PHASE(5);
-  uint32_t kd[8], sd[8];
+  uint64_t h[8];
+  sha512_msg<16>(h, pre, len, msgword);
+  uint32_t hw[16];
+  sha512_digest_words(hw, h);
+  sc_reduce512(k, hw);
   sc_recode8(kd, k);
-  sc_recode16(sd, Sw);
-  auto adig = [&](int i) -> int { return (int)((sel8(kd, i >> 2) >> (8 * (i & 3))) & 255) - 128; };
-  auto bdig = [&](int i) -> int { return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000; };
-  AT2V_PHASE(2);
-  // V4: R' = sum of the 32 A entries, then the 16 B entries; entry m + 1 is fetched while entry m is added
-  gu_p3 acc;
+}
+
+AT2V_HD AT2V_INLINE int comb_adigit(const uint32_t kd[8], int i) {
+  return (int)((sel8(kd, i >> 2) >> (8 * (i & 3))) & 255) - 128;
+}
+AT2V_HD AT2V_INLINE int comb_bdigit(const uint32_t sd[8], int i) {
+  return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000;
+}
+
+// acc += sum over positions i in [i0, i1) of the signed entry C[i][e_i] (A comb, cached form, kAComb) or D[i][f_i] (B
+// comb, affine Niels). i1 - i0 even; the entry of addition m + 1 is fetched (into the other stage) while m is computed.
+template <bool kAComb, class Tab>
+AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int i1, const Tab& tab) {
+  auto digit = [&](int i) {
+    if constexpr (kAComb) return comb_adigit(dig, i);
+    else return comb_bdigit(dig, i);
+  };
   gu_p1p1 t;
-  gu_cached ca;
-  gu_niels nb;
-  gu_p3_identity(acc);
-  int e = adig(0);
-  tc.prefetch(0, 0, e < 0 ? -e : e);
+  int e = digit(i0);
+  tab.prefetch(0, i0, e < 0 ? -e : e);
 #pragma unroll 1
-  for (int i = 0; i < kCombPos; i += 2) {
+  for (int i = i0; i < i1; i += 2) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // stage h holds entry i + h
       const int m = i + h;
-      const int en = m + 1 < kCombPos ? adig(m + 1) : bdig(0);
-      tc.load_prefetched(h, ca);
-      if (m + 1 < kCombPos)
-        tc.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
-      else
-        tb.prefetch(h ^ 1, 0, en < 0 ? -en : en);
-      gu_cached_cneg(ca, e < 0);
-      gu_add(t, acc, ca);
+      const int en = m + 1 < i1 ? digit(m + 1) : 0;
+      if constexpr (kAComb) {
+        gu_cached ca;
+        tab.load_prefetched(h, ca);
+        if (m + 1 < i1) tab.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
+        gu_cached_cneg(ca, e < 0);
+        gu_add(t, acc, ca);
+      } else {
+        gu_niels nb;
+        tab.load_prefetched(h, nb);
+        if (m + 1 < i1) tab.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
+        gu_niels_cneg(nb, e < 0);
+        gu_madd(t, acc, nb);
+      }
       gu_p1p1_to_p3(acc, t);
       e = en;
     }
   }
-#pragma unroll 1
-  for (int i = 0; i < kBCombPos; i += 2) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // the last A entry sat in stage 1, so B entry i + h is in stage h
-      const int m = i + h;
-      const int en = m + 1 < kBCombPos ? bdig(m + 1) : 0;
-      tb.load_prefetched(h, nb);
-      if (m + 1 < kBCombPos) tb.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
-      gu_niels_cneg(nb, e < 0);
-      gu_madd(t, acc, nb);
-      if (m + 1 < kBCombPos) gu_p1p1_to_p3(acc, t);
-      e = en;
-    }
-  }
+}
+
+// dalek-1.x verify of one record from the comb of its key (one lane per record: the throughput path).
+template <class TabC, class TabBC, class MsgWord>
+AT2V_HD AT2V_INLINE int verify_comb_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                       MsgWord msgword, int policy, int a_ok, const TabC& tc, const TabBC& tb) {
+  const int ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
+  uint32_t kd[8], sd[8];
+  comb_k_digits(kd, Rw, Aw, len, msgword);
+  sc_recode16(sd, Sw);
+  AT2V_PHASE(2);
+  // V4: R' = [k](-A) + [s]B as the sum of the 32 A entries and the 16 B entries
+  gu_p3 acc;
+  gu_p3_identity(acc);
+  comb_sum<true>(acc, kd, 0, kCombPos, tc);
+  comb_sum<false>(acc, sd, 0, kBCombPos, tb);
   AT2V_PHASE(4);
   // V5/V6: dalek compares the compressed R' with the 32 bytes of R
   gu_p2 Rp;
-  gu_p1p1_to_p2(Rp, t);
+  gu_p3_to_p2(Rp, acc);
   return ok & gu_encode_eq(Rp, Rw);
+}
+
+// The low-latency split (verify_comb_lat_kernel: one wave per part, on different SIMDs): R decoded on its own instead
+// of R' encoded (no inversion after the sums), R' = Pa0 + Pa1 + Pb from the partial sums, compared projectively.
+// enc(R') == R_bytes <=> R_bytes is canonical (y < p, not x = 0 with the sign bit set), decodes, and dec(R_bytes) = R'
+// (DESIGN.md §4b step 5), so the verdict is dalek's.
+AT2V_HD AT2V_INLINE int comb_decode_r(gu_p3& R, const uint32_t Rw[8]) {
+  int ok = gu_frombytes(R, Rw);
+  ok &= enc_y_canonical(Rw);
+  ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
+  return ok;
+}
+AT2V_HD AT2V_INLINE int comb_check_split(const gu_p3& R, const gu_p3& Pa0, const gu_p3& Pa1, const gu_p3& Pb) {
+  gu_cached c;
+  gu_p1p1 t;
+  gu_p3 S;
+  gu_p3_to_cached(c, Pa1);
+  gu_add(t, Pa0, c);
+  gu_p1p1_to_p3(S, t);
+  gu_p3_to_cached(c, Pb);
+  gu_add(t, S, c);
+  gu_p2 P;
+  gu_p1p1_to_p2(P, t);
+  // R = (x, y, 1, xy): X = x Z and Y = y Z
+  fu u, d;
+  fu_mulc(u, R.X, P.Z);
+  fu_sub(d, P.X, u, FU_KC);
+  const int ex = fu_iszero(d);
+  fu_mulc(u, R.Y, P.Z);
+  fu_sub(d, P.Y, u, FU_KC);
+  return ex & fu_iszero(d);
 }
 
 // One lane's share of the comb of key A: position pos (0..31), half h (0..1) -> entries j = 64h + 1 .. 64h + 64 of

@@ -602,6 +602,123 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
                       slot_of, cache, cache_ctl);
 }
 
+// Low-latency verify from combs (at2v_opts.sender_comb, launches of <= small_batch_max records): a block of 4 waves (one
+// per SIMD) owns a chunk of 64 records and splits each record's work by wave (at2v_comb.h, comb_check_split):
+//   wave 0: decode R and check its canonicity (one exponentiation), then, after the barrier, R' = Pa0 + Pa1 + Pb and
+//           the projective comparison -> verdict words
+//   wave 1: s < l, the 16 B-comb additions -> Pb
+//   wave 2: SHA-512 -> k, A-comb positions 0..15 -> Pa0;   wave 3: SHA-512 -> k, positions 16..31 -> Pa1
+// so a record's latency is the longest part (SHA-512 + 16 additions) instead of SHA-512 + 48 additions + an inversion.
+// A chunk whose records do not all hit the cache (claims beyond the capacity, probe failures) runs the uncached half-size
+// path on wave 0. Verdict words are written by wave 0's lane 0 for every chunk.
+constexpr int kLatBlock = 256;
+__global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int* __restrict__ slot_of,
+    const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl, const int4* __restrict__ comb,
+    const int4* __restrict__ bcomb) {
+  __shared__ int4 stage[4 * 2 * 640];        // per wave two 10 KiB LDS-DMA stages
+  __shared__ uint32_t part[3 * 40 * 64];      // Pb, Pa0, Pa1 (p3, 40 words) per lane, word-major
+  __shared__ uint32_t sok[64];                // wave 1's s < l
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int4* st0 = stage + (size_t)w * 2 * 640;
+  int4* st1 = st0 + 640;
+  const uint32_t nchunks = (n + 63) / 64, nwords = (n + 31) / 32;
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint32_t i = c * 64 + lane;
+    const uint32_t ii = i < n ? i : n - 1;
+    uint32_t Rw[8], Sw[8], Aw[8];
+    load8(Rw, sig + (size_t)ii * 64);
+    load8(Sw, sig + (size_t)ii * 64 + 32);
+    load8(Aw, pk + (size_t)ii * 32);
+    int a_ok = 0, comb_idx = 0;
+    const bool hit = cache_hit(cache, slot_of[ii], Aw, a_ok, comb_idx);
+    const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);  // the same records in every wave
+    if (w == 0 && lane == 0) {
+      atomicAdd(cache_ctl + kCtlChunks, 1ull);
+      if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 1ull);
+    }
+    const uint32_t o0 = off[ii];
+    const uint32_t len = off[ii + 1] - o0;
+    const int msg_fast =
+        __builtin_amdgcn_readfirstlane(__all((uint64_t)o0 + len + 8 <= (uint64_t)msg_total) ? 1 : 0);
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (o0 >> 2);
+    const uint32_t msh = (o0 & 3u) * 8;
+    auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
+    auto msg_guarded = [=](uint32_t j) -> uint32_t {
+      const uint32_t a = o0 + 4 * j;
+      const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+      const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+      if (sh == 0) return lo;
+      const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+      return __builtin_amdgcn_alignbit(hi, lo, sh);
+    };
+    auto touched = [] {};
+    MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> msgword{msg_fast, msg_unguarded,
+                                                                                        msg_guarded, touched};
+    int good = 0;
+    if (all_hit) {
+      gu_p3 R;
+      int ok0 = 0;
+      if (w == 0) {
+        ok0 = comb_decode_r(R, Rw) & comb_prechecks(Rw, Aw, Sw, policy, a_ok);
+      } else {
+        gu_p3 P;
+        gu_p3_identity(P);
+        if (w == 1) {
+          sok[lane] = (uint32_t)sc_is_canonical(Sw);
+          uint32_t sd[8];
+          sc_recode16(sd, Sw);
+          const DevBComb tb{bcomb, {st0, st1}, lane};
+          comb_sum<false>(P, sd, 0, kBCombPos, tb);
+        } else {
+          uint32_t kd[8];
+          comb_k_digits(kd, Rw, Aw, len, msgword);
+          const DevComb tc{comb + (size_t)comb_idx * (kCombBytes / 16), {st0, st1}, lane};
+          comb_sum<true>(P, kd, w == 2 ? 0 : kCombPos / 2, w == 2 ? kCombPos / 2 : kCombPos, tc);
+        }
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(&P);
+        uint32_t* dst = part + (size_t)(w - 1) * 40 * 64;
+#pragma unroll
+        for (int q = 0; q < 40; ++q) dst[q * 64 + lane] = pw[q];
+      }
+      __syncthreads();
+      if (w == 0) {
+        gu_p3 Pb, Pa0, Pa1;
+        uint32_t* pb = reinterpret_cast<uint32_t*>(&Pb);
+        uint32_t* p0 = reinterpret_cast<uint32_t*>(&Pa0);
+        uint32_t* p1 = reinterpret_cast<uint32_t*>(&Pa1);
+#pragma unroll
+        for (int q = 0; q < 40; ++q) {
+          pb[q] = part[q * 64 + lane];
+          p0[q] = part[40 * 64 + q * 64 + lane];
+          p1[q] = part[80 * 64 + q * 64 + lane];
+        }
+        good = ok0 & (int)sok[lane] & comb_check_split(R, Pa0, Pa1, Pb) & (i < n);
+      }
+      __syncthreads();  // the LDS parts are reused by the block's next chunk
+    } else if (w == 0) {
+      int4* slot = scratch + ((size_t)blockIdx.x * kWavesPerBlock * 64 + lane) * kLaneGranules;
+      const int4* ident = btab + (size_t)kNumBtabs * kBtabEntries * 8;
+      DevTabA ta{slot, st0, lane, ident};
+      DevTabA tr{slot + kTabAGranules, st1, lane, ident};
+      const DevTabB tb0{btab, st0, lane};
+      const DevTabB tb1{btab + (size_t)kBtabEntries * 8, st1, lane};
+      auto wmax = [](int v) { return wave_max_i32(v); };
+      good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax) & (i < n);
+    }
+    if (w == 0) {
+      const uint64_t mask = __ballot(good);
+      if (lane == 0) {
+        verdicts[2 * c] = (uint32_t)mask;
+        if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
+      }
+    }
+  }
+}
+
 // the same with per-key combs (at2v_opts.sender_comb): all-hit waves verify by additions only
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -1291,6 +1408,13 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   if (cache) {
     const hipError_t ce = launch_cache_prepare(*cache, pk, n, stream);
     if (ce != hipSuccess) return ce;
+    if (cache->comb && n <= pair_max) {  // small batches: the four-wave split, one block per 64 records
+      const uint32_t gl = nchunks < (uint32_t)grid ? nchunks : (uint32_t)grid;
+      hipLaunchKernelGGL(verify_comb_lat_kernel, dim3(gl), dim3(kLatBlock), 0, stream, pk, sig, msg, msg_total, off, n,
+                         policy, verdicts, scratch, btab, cache->slot_of, (const int4*)cache->entries, cache->ctl,
+                         (const int4*)cache->comb, cache->bcomb);
+      return hipGetLastError();
+    }
     if (cache->comb) {
       hipLaunchKernelGGL(verify_kernel_comb, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
                          verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl,

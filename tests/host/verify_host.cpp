@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
   size_t bad_d = 0, bad_s = 0;
   int limit = argc > 2 ? atoi(argv[2]) : (int)n;
   // 1: the half-size equation (verify_half); 2: on the unsigned field; 3: two lanes per signature (verify_pair_part);
-  // 4: from per-key combs (verify_comb_fu, the sender-comb path)
+  // 4: from per-key combs (verify_comb_fu, the sender-comb path); 5: the comb path's low-latency four-wave split
   const int half = argc > 3 ? atoi(argv[3]) : 0;
   std::map<std::vector<uint32_t>, HostComb*> combs;
   HostBComb bcomb;
@@ -185,7 +185,28 @@ int main(int argc, char** argv) {
     static HostTabB16 tb;
     HostTabA ta, tr;
     int d, s;
-    if (half == 4) {
+    if (half == 5) {  // the low-latency kernel's four-way split (comb_decode_r | B sum | A sums) and comb_check_split
+      std::vector<uint32_t> key(A, A + 8);
+      auto it = combs.find(key);
+      if (it == combs.end()) it = combs.emplace(key, new HostComb(A)).first;
+      const HostComb& c = *it->second;
+      auto split = [&](int policy) {
+        gu_p3 Rp, Pb, Pa0, Pa1;
+        const int ok0 = comb_decode_r(Rp, R) & comb_prechecks(R, A, S, policy, c.a_ok);
+        uint32_t sd[8], kd[8];
+        sc_recode16(sd, S);
+        gu_p3_identity(Pb);
+        comb_sum<false>(Pb, sd, 0, kBCombPos, bcomb);
+        comb_k_digits(kd, R, A, len, mw);
+        gu_p3_identity(Pa0);
+        gu_p3_identity(Pa1);
+        comb_sum<true>(Pa0, kd, 0, kCombPos / 2, c);
+        comb_sum<true>(Pa1, kd, kCombPos / 2, kCombPos, c);
+        return ok0 & comb_check_split(Rp, Pa0, Pa1, Pb);
+      };
+      d = split(POLICY_DALEK_V1);
+      s = split(POLICY_LIBSODIUM_1_0_18);
+    } else if (half == 4) {
       std::vector<uint32_t> key(A, A + 8);
       auto it = combs.find(key);
       if (it == combs.end()) it = combs.emplace(key, new HostComb(A)).first;

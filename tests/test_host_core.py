@@ -29,8 +29,9 @@ def host_exe_asan():
     return exe
 
 
-MODES = [0, 1, 2, 3, 4]
-MODE_IDS = ["full_length", "half_size", "half_size_unsigned_field", "two_lanes_per_record", "sender_comb"]
+MODES = [0, 1, 2, 3, 4, 5]
+MODE_IDS = ["full_length", "half_size", "half_size_unsigned_field", "two_lanes_per_record", "sender_comb",
+            "sender_comb_split"]
 
 
 @pytest.mark.parametrize("half", MODES, ids=MODE_IDS)
@@ -38,7 +39,7 @@ def test_sanitized_host_build_of_device_core(host_exe_asan, half):
     """the same code under AddressSanitizer + UBSan (signed overflow, shifts, bounds) over the edge and
     adversarial fixtures (the comb form on fewer records: every distinct key builds its 4128-entry comb)"""
     for name, limit in (("edge", 3000), ("adversarial", 800)):
-        if half == 4:
+        if half >= 4:
             limit = 40
         out = subprocess.run([host_exe_asan, os.path.join(golden_io.GOLDEN_DIR, name + ".bin"), str(limit), str(half)],
                              capture_output=True, text=True, timeout=900)
@@ -51,9 +52,10 @@ def test_host_build_of_device_core_matches_golden(host_exe, name, half):
     """every verify form the kernels can be built with: the full-length ladder (verify_core), the half-size lattice
     form on the signed field (verify_half) and on the unsigned chained-carry field (verify_half_fu, the throughput
     kernel), its two-lanes-per-record split (verify_pair_part + verify_pair_combine, the low-latency kernel), and the
-    sender-comb form (comb_build_lane + verify_comb_fu, at2v_comb.h; first 1,200 records of a set, since every distinct
-    key builds its comb), against OpenSSL/libsodium-derived verdicts"""
-    limit = "1200" if half == 4 else "1000000"
+    sender-comb form (comb_build_lane + verify_comb_fu, at2v_comb.h) and its low-latency four-wave split (comb_decode_r,
+    comb_sum over the halves, comb_check_split) on the first 1,200 records of a set (every distinct key builds its
+    comb), against OpenSSL/libsodium-derived verdicts"""
+    limit = "1200" if half >= 4 else "1000000"
     out = subprocess.run([host_exe, os.path.join(golden_io.GOLDEN_DIR, name + ".bin"), limit, str(half)],
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
