@@ -48,6 +48,22 @@ AT2V_HD AT2V_INLINE int gu_encode_eq(const gu_p2& P, const uint32_t Rw[8]) {
   return eq;
 }
 
+// enc(P) == R_bytes with 1/Z given (P in p2 or p3: x = X/Z, y = Y/Z)
+template <class P>
+AT2V_HD AT2V_INLINE int gu_encode_eq_zi(const P& p, const fu& zi, const uint32_t Rw[8]) {
+  fu x, y;
+  fu_mulc(x, p.X, zi);
+  fu_mulc(y, p.Y, zi);
+  uint32_t enc[8], xb[8];
+  fu_tobytes(enc, y);
+  fu_tobytes(xb, x);
+  enc[7] ^= (xb[0] & 1u) << 31;
+  int eq = 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) eq &= enc[i] == Rw[i];
+  return eq;
+}
+
 // Checks that need no point arithmetic: V1 (s < l), A's decode verdict (held with the comb), libsodium's pre-rejects.
 AT2V_HD AT2V_INLINE int comb_prechecks(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], int policy,
                                        int a_ok) {
@@ -119,6 +135,18 @@ AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int
       e = en;
     }
   }
+}
+
+// R' = [k](-A) + [s]B of one record from the combs (V3 + V4 of the full-length form): the point, not yet encoded
+template <class TabC, class TabBC, class MsgWord>
+AT2V_HD AT2V_INLINE void comb_point(gu_p3& acc, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
+                                    uint32_t len, MsgWord msgword, const TabC& tc, const TabBC& tb) {
+  uint32_t kd[8], sd[8];
+  comb_k_digits(kd, Rw, Aw, len, msgword);
+  sc_recode16(sd, Sw);
+  gu_p3_identity(acc);
+  comb_sum<true>(acc, kd, 0, kCombPos, tc);
+  comb_sum<false>(acc, sd, 0, kBCombPos, tb);
 }
 
 // dalek-1.x verify of one record from the comb of its key (one lane per record: the throughput path).

@@ -719,6 +719,145 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
   }
 }
 
+// Comb throughput path with two records per lane (at2v_opts.sender_comb): a chunk is 128 records, lane l
+// verifies records 128c + l and 128c + 64 + l. If all 128 hit the cache, both R' come from comb additions and their two
+// inversions share one (Montgomery's trick: 1/Z0 = Z1 / (Z0 Z1), 1/Z1 = Z0 / (Z0 Z1)); otherwise each 64-record half runs
+// the uncached half-size path. Chunks come from the per-launch queue as in verify_chunks.
+__device__ AT2V_INLINE void verify_chunks_comb2(
+    int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
+    uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
+    uint32_t* __restrict__ chunk_queue, const int* __restrict__ slot_of, const int4* __restrict__ cache,
+    unsigned long long* __restrict__ cache_ctl, const int4* __restrict__ comb, const int4* __restrict__ bcomb) {
+  const int lane = threadIdx.x & 63;
+  const int wib = AT2V_UNIFORM(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t nchunks = (n + 127) / 128;
+  const uint32_t nwords = (n + 31) / 32;
+  int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
+  const int4* ident = btab + (size_t)kNumBtabs * kBtabEntries * 8;
+  int4* const sa = astage + wib * 640;
+  int4* const sr = rstage + wib * 640;
+  DevTabA ta{slot, sa, lane, ident};
+  DevTabA tr{slot + kTabAGranules, sr, lane, ident};
+  const DevTabB tb0{btab, sa, lane};
+  const DevTabB tb1{btab + (size_t)kBtabEntries * 8, sr, lane};
+  const DevBComb tbc{bcomb, {sa, sr}, lane};
+  auto wmax = [](int v) { return wave_max_i32(v); };
+  constexpr uint32_t kHalf = kWavesPerBlock / 2;
+  const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
+                                            : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
+  for (uint32_t c = c_first; c < nchunks;) {
+    uint32_t Rw[2][8], Sw[2][8], Aw[2][8], o0[2], len[2];
+    int a_ok[2], cidx[2], hit = 1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t i = c * 128 + 64 * h + lane;
+      const uint32_t ii = i < n ? i : n - 1;
+      load8(Rw[h], sig + (size_t)ii * 64);
+      load8(Sw[h], sig + (size_t)ii * 64 + 32);
+      load8(Aw[h], pk + (size_t)ii * 32);
+      o0[h] = off[ii];
+      len[h] = off[ii + 1] - o0[h];
+      hit &= cache_hit(cache, slot_of[ii], Aw[h], a_ok[h], cidx[h]) ? 1 : 0;
+    }
+    const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
+    if (lane == 0) {
+      atomicAdd(cache_ctl + kCtlChunks, 2ull);
+      if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 2ull);
+    }
+    // message reader of half h (the fast form when the wave's messages all end 8 bytes before the buffer end)
+    auto run = [&](int h, auto&& body) -> int {
+      const uint32_t b0 = o0[h], bl = len[h];
+      const int msg_fast =
+          __builtin_amdgcn_readfirstlane(__all((uint64_t)b0 + bl + 8 <= (uint64_t)msg_total) ? 1 : 0);
+      const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (b0 >> 2);
+      const uint32_t msh = (b0 & 3u) * 8;
+      auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
+      auto msg_guarded = [=](uint32_t j) -> uint32_t {
+        const uint32_t a = b0 + 4 * j;
+        const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+        const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+        if (sh == 0) return lo;
+        const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+        return __builtin_amdgcn_alignbit(hi, lo, sh);
+      };
+      auto touched = [] {};
+      MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> msgword{msg_fast, msg_unguarded,
+                                                                                          msg_guarded, touched};
+      return body(msgword);
+    };
+    int good[2];
+    if (all_hit) {
+      gu_p3 P0, P1;
+      run(0, [&](auto& mwd) {
+        const DevComb tc{comb + (size_t)cidx[0] * (kCombBytes / 16), {sa, sr}, lane};
+        comb_point(P0, Rw[0], Aw[0], Sw[0], len[0], mwd, tc, tbc);
+        return 0;
+      });
+      run(1, [&](auto& mwd) {
+        const DevComb tc{comb + (size_t)cidx[1] * (kCombBytes / 16), {sa, sr}, lane};
+        comb_point(P1, Rw[1], Aw[1], Sw[1], len[1], mwd, tc, tbc);
+        return 0;
+      });
+      fu zz, inv, zi;
+      fu_mulc(zz, P0.Z, P1.Z);
+      fu_invert(inv, zz);
+      fu_mulc(zi, inv, P1.Z);
+      good[0] = comb_prechecks(Rw[0], Aw[0], Sw[0], policy, a_ok[0]) & gu_encode_eq_zi(P0, zi, Rw[0]);
+      fu_mulc(zi, inv, P0.Z);
+      good[1] = comb_prechecks(Rw[1], Aw[1], Sw[1], policy, a_ok[1]) & gu_encode_eq_zi(P1, zi, Rw[1]);
+    } else {
+      // one half at a time through ONE inlined copy of the ladder: the half's words are selected into plain arrays
+      // (a runtime index into Rw[2][8] would put the arrays in scratch)
+#pragma unroll 1
+      for (int h = 0; h < 2; ++h) {
+        uint32_t R1[8], A1[8], S1[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          R1[q] = h ? Rw[1][q] : Rw[0][q];
+          A1[q] = h ? Aw[1][q] : Aw[0][q];
+          S1[q] = h ? Sw[1][q] : Sw[0][q];
+        }
+        const uint32_t b0 = h ? o0[1] : o0[0], bl = h ? len[1] : len[0];
+        const int msg_fast =
+            __builtin_amdgcn_readfirstlane(__all((uint64_t)b0 + bl + 8 <= (uint64_t)msg_total) ? 1 : 0);
+        const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (b0 >> 2);
+        const uint32_t msh = (b0 & 3u) * 8;
+        auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
+        auto msg_guarded = [=](uint32_t j) -> uint32_t {
+          const uint32_t a = b0 + 4 * j;
+          const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+          const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+          if (sh == 0) return lo;
+          const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+          return __builtin_amdgcn_alignbit(hi, lo, sh);
+        };
+        auto touched = [] {};
+        MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> mwd{msg_fast, msg_unguarded,
+                                                                                        msg_guarded, touched};
+        const int g = verify_half_fu(R1, A1, S1, bl, mwd, policy, ta, tr, tb0, tb1, wmax);
+        if (h) good[1] = g;
+        else good[0] = g;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t mask = __ballot(good[h] & (c * 128 + 64 * h + lane < n));
+      const uint32_t w0 = 4 * c + 2 * h;
+      if (lane == 0) {
+        if (w0 < nwords) verdicts[w0] = (uint32_t)mask;
+        if (w0 + 1 < nwords) verdicts[w0 + 1] = (uint32_t)(mask >> 32);
+      }
+    }
+    uint32_t ticket = 0;
+    if (lane == 0) ticket = atomicAdd(chunk_queue, 1u);
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    c = ticket < nchunks ? nwaves + ticket : nchunks;
+  }
+}
+
 // the same with per-key combs (at2v_opts.sender_comb): all-hit waves verify by additions only
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -728,8 +867,16 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     const int4* __restrict__ comb, const int4* __restrict__ bcomb) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+#ifndef AT2V_COMB_PAIRS
+#define AT2V_COMB_PAIRS 1  // 1: two records per lane, one shared inversion (verify_chunks_comb2); 0: one record per lane
+#endif
+#if AT2V_COMB_PAIRS
+  verify_chunks_comb2(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
+                      slot_of, cache, cache_ctl, comb, bcomb);
+#else
   verify_chunks<true, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
                             chunk_queue, slot_of, cache, cache_ctl, comb, bcomb);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1416,7 +1563,13 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
       return hipGetLastError();
     }
     if (cache->comb) {
-      hipLaunchKernelGGL(verify_kernel_comb, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+#if AT2V_COMB_PAIRS
+      const uint32_t need2 = ((n + 127) / 128 + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);  // 128-record chunks
+      const int g2 = (int)((uint32_t)grid < need2 ? (uint32_t)grid : need2);
+#else
+      const int g2 = g;
+#endif
+      hipLaunchKernelGGL(verify_kernel_comb, dim3(g2), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
                          verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl,
                          (const int4*)cache->comb, cache->bcomb);
       return hipGetLastError();

@@ -59,6 +59,9 @@ def parse():
                     help="max records for the CPU baseline sample (0 = skip); sized to ~3 s on the threads used")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
     ap.add_argument("--e2e", type=int, default=1, help="1 = also time the host-buffer path (H2D + verify + D2H)")
+    ap.add_argument("--traffic-leg", type=int, default=1,
+                    help="1 = at N=1 also time AT2 traffic (the same records per step, signed by 64 repeating senders) "
+                         "through per-sender combs (at2v_opts.sender_comb); reported as at2_traffic, not as value")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only (tests): the launcher and gloo control plane with oracle verdicts, no GPU")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
@@ -347,6 +350,8 @@ def main():
         }
         if e2e:
             out.update(e2e)
+    if rank == 0 and world == 1 and args.traffic_leg and not args.senders and not use_dist:
+        out["at2_traffic"] = at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args, d_pk, d_sig, d_msg, n, L)
     if rank == 0 and world == 1 and args.pmc_traffic and not use_dist:
@@ -369,6 +374,43 @@ def main():
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
+    """AT2 traffic: n records per step signed by `senders` repeating keys (record i by sender
+    i % senders), verified through a context with the per-sender cache and combs; the combs are built by the first
+    (warm-up) launch. Same step structure as the headline (overlapped launches on the two streams). Reported beside the
+    headline value, which stays the distinct-key workload of BASELINE config 2."""
+    v = at2v.BatchVerifier(device=dev.index or 0, policy=args.policy, sender_cache=1024, sender_comb=True)
+    bufs = [torch.empty(n * 32, dtype=torch.uint8, device=dev), torch.empty(n * 64, dtype=torch.uint8, device=dev),
+            torch.empty(n * L, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int32, device=dev)]
+    vers = [torch.zeros(n // 32, dtype=torch.int32, device=dev) for _ in lstreams]
+    v.gen_records_device(CFG_SEED, 0, n, L, *(b.data_ptr() for b in bufs), lstreams[0].cuda_stream, senders=senders)
+    torch.cuda.synchronize(dev)
+    ptrs = [b.data_ptr() for b in bufs]
+
+    def step(k):
+        j = k % 2
+        v.verify_batch_device(ptrs[0], ptrs[1], ptrs[2], n * L, ptrs[3], n, vers[j].data_ptr(), lstreams[j].cuda_stream)
+
+    for k in range(2):
+        step(k)
+    torch.cuda.synchronize(dev)
+    steps = max(2, args.steps)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ok = all(bool((x == -1).all().item()) for x in vers)
+    info = v.info()
+    v.close()
+    return {"value": n * steps / dt, "unit": "verifies/s", "records_per_step": n, "senders": senders, "steps": steps,
+            "ms_per_step": dt * 1e3 / steps, "verdicts_ok": ok, "cache_chunk_hits": info["cache_chunk_hits"],
+            "cache_chunks": info["cache_chunks"],
+            "method": f"{n} records per step (100-byte M) signed by {senders} repeating senders (GPU generator, record i "
+                      f"by sender i % {senders}), sender_cache 1024 + sender_comb: chunks whose senders are all cached "
+                      "verify by comb additions (DESIGN §10d); combs built in the warm-up"}
 
 
 def dry_run(args, rank, world, use_dist, dist, torch, np):
@@ -483,7 +525,7 @@ def _pmc_pass(args, n, L, counters):
            "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "0",
            "--cpu-sample", "0", "--pmc-traffic", "0", "--records-per-gpu", str(n), "--msg-len", str(L),
            "--policy", args.policy, "--senders", str(args.senders), "--sender-cache", str(args.sender_cache),
-           "--sender-comb", str(args.sender_comb), "--e2e", "0"]
+           "--sender-comb", str(args.sender_comb), "--e2e", "0", "--traffic-leg", "0"]
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150, check=True)
         rows, durs = [], []

@@ -168,7 +168,7 @@ int main(int argc, char** argv) {
   // 1: the half-size equation (verify_half); 2: on the unsigned field; 3: two lanes per signature (verify_pair_part);
   // 4: from per-key combs (verify_comb_fu, the sender-comb path); 5: the comb path's low-latency four-wave split
   const int half = argc > 3 ? atoi(argv[3]) : 0;
-  std::map<std::vector<uint32_t>, HostComb*> combs;
+  std::map<std::vector<uint32_t>, HostComb> combs;
   HostBComb bcomb;
   for (size_t i = 0; i < n && (int)i < limit; ++i) {
     uint32_t R[8], A[8], S[8];
@@ -188,8 +188,8 @@ int main(int argc, char** argv) {
     if (half == 5) {  // the low-latency kernel's four-way split (comb_decode_r | B sum | A sums) and comb_check_split
       std::vector<uint32_t> key(A, A + 8);
       auto it = combs.find(key);
-      if (it == combs.end()) it = combs.emplace(key, new HostComb(A)).first;
-      const HostComb& c = *it->second;
+      if (it == combs.end()) it = combs.try_emplace(key, A).first;
+      const HostComb& c = it->second;
       auto split = [&](int policy) {
         gu_p3 Rp, Pb, Pa0, Pa1;
         const int ok0 = comb_decode_r(Rp, R) & comb_prechecks(R, A, S, policy, c.a_ok);
@@ -209,8 +209,8 @@ int main(int argc, char** argv) {
     } else if (half == 4) {
       std::vector<uint32_t> key(A, A + 8);
       auto it = combs.find(key);
-      if (it == combs.end()) it = combs.emplace(key, new HostComb(A)).first;
-      const HostComb& c = *it->second;
+      if (it == combs.end()) it = combs.try_emplace(key, A).first;
+      const HostComb& c = it->second;
       d = verify_comb_fu(R, A, S, len, mw, POLICY_DALEK_V1, c.a_ok, c, bcomb);
       s = verify_comb_fu(R, A, S, len, mw, POLICY_LIBSODIUM_1_0_18, c.a_ok, c, bcomb);
     } else if (half == 3) {

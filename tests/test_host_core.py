@@ -13,20 +13,26 @@ SRC = os.path.join(ROOT, "tests", "host", "verify_host.cpp")
 EXE = os.path.join(ROOT, "tests", "host", "verify_host")
 
 
+def _build(cmd, exe):
+    """compile to a per-process name, then rename into place: parallel test workers (pytest -n) never execute a file
+    another worker is still writing"""
+    tmp = f"{exe}.{os.getpid()}"
+    subprocess.run(cmd + ["-o", tmp], check=True)
+    os.replace(tmp, exe)
+    return exe
+
+
 @pytest.fixture(scope="module")
 def host_exe():
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC, "-o", EXE],
-                   check=True)
-    return EXE
+    return _build(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC], EXE)
 
 
 @pytest.fixture(scope="module")
 def host_exe_asan():
     exe = EXE + "_asan"
     # -O0: the always-inline field code takes minutes to compile at -O1 under the sanitizers
-    subprocess.run(["g++", "-O0", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-                    "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC, "-o", exe], check=True)
-    return exe
+    return _build(["g++", "-O0", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                   "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC], exe)
 
 
 MODES = [0, 1, 2, 3, 4, 5]
