@@ -98,7 +98,8 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
  * msg buffer in bytes (>= msg_off[n]); d_pk/d_sig 16-byte aligned, d_msg_off/d_verdicts 4-byte aligned.
  * Returns after the launch; results are valid once the stream reaches this point. The ceil(n/32) verdict
  * words are zeroed on the stream before the kernel runs. The launch first waits (on the device, not the
- * host) for the context's previous launch, which may be on another stream. */
+ * host) for the launch that last used the scratch set it takes (a device has two, used in turn), which may be on
+ * another stream: launches on two streams overlap, launches on one stream are ordered by it. */
 int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                              size_t msg_bytes, const uint32_t* d_msg_off, size_t n, uint32_t* d_verdicts,
                              void* hip_stream);
@@ -106,9 +107,9 @@ int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* 
 /* One signature on the CPU, synchronous: 1 = valid, 0 = invalid, < 0 = error. The drop-in for the
  * per-signature `Signature::verify(&message, &public_key)` that drop exposes and sieve/murmur call per payload
  * ("CPU, 1/0"), for callers that verify one payload at a time, e.g. the A/sig decode at
- * rpc.rs:265-281. DALEK_V1 semantics, the product's own field/group/scalar headers (csrc/) compiled for the
- * host; needs no GPU, no context and no lock; reentrant. It is not a fallback of the batch entry points:
- * they never verify on the CPU. */
+ * rpc.rs:265-281. DALEK_V1 semantics: the throughput kernel's own verify routine (csrc/at2v_verify_fu.h)
+ * compiled for the host; needs no GPU, no context and no lock; reentrant (the first call of a process builds the
+ * fixed-base tables, ~30 ms). It is not a fallback of the batch entry points: they never verify on the CPU. */
 int at2v_verify_one(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len);
 /* Same, with an explicit policy (AT2V_POLICY_*). */
 int at2v_verify_one_policy(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len, int policy);
