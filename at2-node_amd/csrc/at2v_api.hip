@@ -247,9 +247,12 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
                         bool zero_verdicts = true) {
   const int j = (int)(s.next_set++ % (unsigned)s.sets);
   hipError_t e = hipStreamWaitEvent(stream, s.scratch_free[j], 0);
-  if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
   // the cache serves the throughput kernel (launches above small_batch_max records; with combs, every launch)
   SenderCache* c = (s.cache && (n > ctx->pair_max || s.cache->args.comb)) ? s.cache : nullptr;
+  // the four-wave comb kernel of small batches writes every verdict word of the launch whatever the verdicts (its
+  // blocks stride over all chunks), so the zeroing is left out there: one dependent memset less on the latency path
+  if (c && c->args.comb && n <= ctx->pair_max) zero_verdicts = false;
+  if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
   if (e == hipSuccess && c) e = hipStreamWaitEvent(stream, c->free, 0);
   if (e == hipSuccess && c) e = cache_before_launch(*c, n, stream);
   if (e == hipSuccess)

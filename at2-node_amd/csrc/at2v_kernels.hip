@@ -1389,9 +1389,8 @@ __global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __rest
   if (claimed) c.new_list[nbase + rank] = make_uint4((uint32_t)slot, i, (uint32_t)(ubase + rank), 0u);
 }
 
-// One lane per entry claimed by this launch: key, dalek decode verdict and [j]A (build_a_table, the verify kernel's own
-// steps), or, with combs on, the key and verdict only (cache_comb_kernel builds the comb). A claim beyond the capacity
-// is written invalid. Threads beyond the launch's claim count leave at once.
+// One lane per entry claimed by this launch (combs off): key, dalek decode verdict and [j]A (build_a_table, the verify
+// kernel's own steps). A claim beyond the capacity is written invalid. Threads beyond the launch's claim count leave.
 __global__ __launch_bounds__(256) void cache_build_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   if ((unsigned long long)t >= __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -1403,38 +1402,43 @@ __global__ __launch_bounds__(256) void cache_build_kernel(const uint8_t* __restr
   }
   uint32_t a[8];
   load8(a, pk + (size_t)e.y * 32);
-  int ok;
-  if (c.comb) {
-    gu_p3 A;
-    ok = gu_frombytes(A, a);
-  } else {
-    DevTabA tw{ent + 3, nullptr, 0, nullptr};  // store() only
-    ok = build_a_table(a, tw);
-  }
+  DevTabA tw{ent + 3, nullptr, 0, nullptr};  // store() only
+  const int ok = build_a_table(a, tw);
   ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
   ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
   ent[2] = make_int4(ok, 1, (int)e.z, 0);
 }
 
-// One wave per entry claimed (and built) by this launch: the comb of -A at claim index u (comb_build_lane, lane =
-// position x half). Persistent grid over the launch's claims.
+// With combs on, the whole build of a launch's claims: one wave per claim (persistent grid) writes the comb of -A at claim
+// index u (comb_build_lane, lane = position x half) and, from lane 0, the entry's key and meta (dalek's decode verdict,
+// valid, u); a claim beyond the capacity is written invalid. (One kernel instead of cache_build_kernel + this one: one
+// dependent launch less per batch, which the small-batch latency pays.)
 __global__ __launch_bounds__(256) void cache_comb_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * 4;
   const unsigned long long cnt = __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < cnt; t += nw) {
     const uint4 e = c.new_list[t];
-    if (e.z >= c.capacity) continue;  // wave-uniform
+    int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
+    if (e.z >= c.capacity) {  // wave-uniform
+      if (lane == 0) ent[2] = make_int4(0, 0, 0, 0);
+      continue;
+    }
     uint32_t a[8];
     load8(a, pk + (size_t)e.y * 32);
     int4* cb = c.comb + (size_t)e.z * (kCombBytes / 16);
     const int pos = lane >> 1;
-    comb_build_lane(a, pos, lane & 1, [&](int j, const gu_cached& p) {
+    const int ok = comb_build_lane(a, pos, lane & 1, [&](int j, const gu_cached& p) {
       const int32_t* w = reinterpret_cast<const int32_t*>(&p);
       int4* dst = cb + ((size_t)pos * kCombEntries + j) * kCombGranules;
 #pragma unroll
       for (int q = 0; q < kCombGranules; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     });
+    if (lane == 0) {
+      ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
+      ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
+      ent[2] = make_int4(ok, 1, (int)e.z, 0);
+    }
   }
 }
 
@@ -1497,13 +1501,13 @@ hipError_t launch_cache_prepare(const CacheArgs& c, const uint8_t* pk, uint32_t 
   hipLaunchKernelGGL(cache_lookup_kernel, dim3(blocks), dim3(256), 0, stream, pk, n, c);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(cache_build_kernel, dim3(blocks), dim3(256), 0, stream, pk, c);
-  e = hipGetLastError();
-  if (e != hipSuccess || !c.comb) return e;
-  // one wave per claim; claims of a launch <= its records, and <= the capacity get built
-  const uint32_t waves = n < c.capacity ? n : c.capacity;
-  const uint32_t cblocks = ((waves < 2048u ? waves : 2048u) + 3) / 4;
-  hipLaunchKernelGGL(cache_comb_kernel, dim3(cblocks), dim3(256), 0, stream, pk, c);
+  if (!c.comb) {
+    hipLaunchKernelGGL(cache_build_kernel, dim3(blocks), dim3(256), 0, stream, pk, c);
+    return hipGetLastError();
+  }
+  // one wave per claim; a launch claims at most n entries (waves loop over more)
+  const uint32_t waves = n < 2048u ? n : 2048u;
+  hipLaunchKernelGGL(cache_comb_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, pk, c);
   return hipGetLastError();
 }
 
@@ -1547,10 +1551,14 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   const uint32_t nchunks = (n + 63) / 64;
   const uint32_t need_blocks = (nchunks + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);  // half-filled blocks
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
-  // chunk queue counter: the word after the `grid` blocks' lane slots (scratch_bytes(grid))
+  // chunk queue counter: the word after the `grid` blocks' lane slots (scratch_bytes(grid)); the four-wave comb kernel of
+  // small batches strides over its chunks and needs none (one dependent memset less on the latency path)
   uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesPerBlock);
-  const hipError_t me = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
-  if (me != hipSuccess) return me;
+  const bool lat_comb = cache && cache->comb && n <= pair_max;
+  if (!lat_comb) {
+    const hipError_t me = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+    if (me != hipSuccess) return me;
+  }
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
   if (cache) {
     const hipError_t ce = launch_cache_prepare(*cache, pk, n, stream);
