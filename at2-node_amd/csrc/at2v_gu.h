@@ -13,6 +13,26 @@
 
 namespace at2v {
 
+// AT2V_GU_X2 = 1: the group law's independent products run as interleaved pairs (two MAD chains in one asm block);
+// 0: one product at a time through the single-product variants (same columns; the pair's one-MAD wraps become the single
+// functions' own wraps, always valid) — fewer live registers at the price of less ILP (A/B, profiles/r03q).
+#ifndef AT2V_GU_X2
+#define AT2V_GU_X2 1
+#endif
+#if AT2V_GU_X2
+#define GU_MUL_WN(a, f0, g0, b, f1, g1) fu_mul_wn(a, f0, g0, b, f1, g1)
+#define GU_MUL_NN(a, f0, g0, b, f1, g1) fu_mul_nn(a, f0, g0, b, f1, g1)
+#define GU_MUL_X2(a, f0, g0, b, f1, g1) fu_mul_x2(a, f0, g0, b, f1, g1)
+#define GU_SQC_X2(a, f0, b, f1) fu_sqc_x2(a, f0, b, f1)
+#define GU_SQ_SQ2_N(a, f0, b, f1) fu_sq_sq2_n(a, f0, b, f1)
+#else
+#define GU_MUL_WN(a, f0, g0, b, f1, g1) (fu_mul(a, f0, g0), fu_mul_n(b, f1, g1))
+#define GU_MUL_NN(a, f0, g0, b, f1, g1) (fu_mul_n(a, f0, g0), fu_mul_n(b, f1, g1))
+#define GU_MUL_X2(a, f0, g0, b, f1, g1) (fu_mul(a, f0, g0), fu_mul(b, f1, g1))
+#define GU_SQC_X2(a, f0, b, f1) (fu_sqc(a, f0), fu_sqc(b, f1))
+#define GU_SQ_SQ2_N(a, f0, b, f1) (fu_sq(a, f0), fu_sq2(b, f1))
+#endif
+
 struct gu_p2 { fu X, Y, Z; };
 struct gu_p3 { fu X, Y, Z, T; };
 struct gu_p1p1 { fu X, Y, Z, T; };
@@ -27,13 +47,13 @@ AT2V_HD AT2V_INLINE void gu_p3_identity(gu_p3& p) {
 }
 
 AT2V_HD AT2V_INLINE void gu_p1p1_to_p2(gu_p2& r, const gu_p1p1& p) {
-  fu_mul_wn(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  GU_MUL_WN(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fu_mul(r.Z, p.Z, p.T);
 }
 
 AT2V_HD AT2V_INLINE void gu_p1p1_to_p3(gu_p3& r, const gu_p1p1& p) {
-  fu_mul_wn(r.X, p.X, p.T, r.Y, p.Y, p.Z);
-  fu_mul_x2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
+  GU_MUL_WN(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  GU_MUL_X2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
 }
 
 // dbl-2008-hwcd, p2 -> p1p1: XX = X^2, YY = Y^2, ZZ2 = 2 Z^2, t0 = (X+Y)^2;
@@ -42,8 +62,8 @@ AT2V_HD AT2V_INLINE void gu_p1p1_to_p3(gu_p3& r, const gu_p1p1& p) {
 AT2V_HD AT2V_INLINE void gu_p2_dbl(gu_p1p1& r, const gu_p2& p) {
   fu XX, YY, ZZ2, s, t0;
   fu_add(s, p.X, p.Y);
-  fu_sqc_x2(XX, p.X, YY, p.Y);
-  fu_sq_sq2_n(t0, s, ZZ2, p.Z);
+  GU_SQC_X2(XX, p.X, YY, p.Y);
+  GU_SQ_SQ2_N(t0, s, ZZ2, p.Z);
   fu_add(r.Y, XX, YY);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -66,8 +86,8 @@ AT2V_HD AT2V_INLINE void gu_add(gu_p1p1& r, const gu_p3& p, const gu_cached& q) 
   fu a, b, c, d, ym, yp;
   fu_sub(ym, p.Y, p.X, FU_KC);
   fu_add(yp, p.Y, p.X);
-  fu_mul_wn(a, ym, q.YmX, b, yp, q.YpX);
-  fu_mul_nn(c, p.T, q.T2d, d, p.Z, q.Z2);
+  GU_MUL_WN(a, ym, q.YmX, b, yp, q.YpX);
+  GU_MUL_NN(c, p.T, q.T2d, d, p.Z, q.Z2);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     r.X.v[i] = b.v[i] + FU_KC.v[i] - a.v[i];  // E
@@ -82,7 +102,7 @@ AT2V_HD AT2V_INLINE void gu_madd(gu_p1p1& r, const gu_p3& p, const gu_niels& q) 
   fu a, b, c, ym, yp;
   fu_sub(ym, p.Y, p.X, FU_KC);
   fu_add(yp, p.Y, p.X);
-  fu_mul_nn(a, ym, q.ymx, b, yp, q.ypx);
+  GU_MUL_NN(a, ym, q.ymx, b, yp, q.ypx);
   fu_mul_n(c, p.T, q.xy2d);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {

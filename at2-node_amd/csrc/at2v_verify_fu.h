@@ -21,6 +21,34 @@ namespace at2v {
 #ifndef AT2V_PARK_POINTS
 #define AT2V_PARK_POINTS 0  // 1: decoded A and R parked in the table slots across SHA-512 / lattice (0: kept live)
 #endif
+// The A and R decodes and the two tables ran as interleaved pairs in round 2. One after the other they hold fewer live
+// values: verify_kernel's spills fall from 146 to 75 VGPRs (scratch 688 -> 464 B/lane) and the kernel runs 2.2% faster
+// (two A/B runs on two boxes, profiles/r03q, r03r). 1 = the round-2 interleaved forms (A/B).
+#ifndef AT2V_DECODE_X2
+#define AT2V_DECODE_X2 0
+#endif
+#ifndef AT2V_TABLES_X2
+#define AT2V_TABLES_X2 0
+#endif
+
+// [j]P, j = 0..8, cached form, into tp (one table; the A/B form of the interleaved build)
+template <class TabP>
+AT2V_HD AT2V_INLINE void build_a_table_from(const gu_p3& P1, TabP& tp) {
+  gu_cached c1, cj;
+  gu_cached_identity(cj);
+  tp.store(0, cj);
+  gu_p3_to_cached(c1, P1);
+  tp.store(1, c1);
+  gu_p3 Q = P1;
+#pragma unroll 1
+  for (int j = 2; j <= 8; ++j) {
+    gu_p1p1 s;
+    gu_add(s, Q, c1);
+    gu_p1p1_to_p3(Q, s);
+    gu_p3_to_cached(cj, Q);
+    tp.store(j, cj);
+  }
+}
 
 template <bool kCacheable = false, class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax,
           class Pace = NoPace>
@@ -39,9 +67,14 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   if (kCacheable && a_cached) {
     ok &= gu_frombytes(R, Rw) & a_cached_ok;
   } else {
+#if AT2V_DECODE_X2
     int okd[2];
     gu_frombytes_x2(A, Aw, R, Rw, okd);
     ok &= okd[0] & okd[1];
+#else
+    ok &= gu_frombytes(A, Aw);
+    ok &= gu_frombytes(R, Rw);
+#endif
   }
   ok &= enc_y_canonical(Rw);
   ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
@@ -91,7 +124,8 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   AT2V_PHASE(2);
   pace.mark(1);
 
-  // tables [j]A and [j](+-R), j = 0..8, built as one interleaved pair
+  // tables [j]A and [j](+-R), j = 0..8: one after the other (AT2V_TABLES_X2 = 0, the default since round 3: the pair's
+  // extra live registers cost more in spills than its ILP gains, profiles/r03q), or as one interleaved pair
 #if AT2V_PARK_POINTS
   if (!(kCacheable && a_cached)) ta.unpark(A);
   tr.unpark(R);
@@ -103,21 +137,9 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     fu_carry(R.T);
   }
   if (kCacheable && a_cached) {  // [j]A comes from the cache entry: build [j](+-R) alone
-    gu_cached cr1, cj;
-    gu_cached_identity(cj);
-    tr.store(0, cj);
-    gu_p3_to_cached(cr1, R);
-    tr.store(1, cr1);
-    gu_p3 PR = R;
-#pragma unroll 1
-    for (int j = 2; j <= 8; ++j) {
-      gu_p1p1 sr;
-      gu_add(sr, PR, cr1);
-      gu_p1p1_to_p3(PR, sr);
-      gu_p3_to_cached(cj, PR);
-      tr.store(j, cj);
-    }
+    build_a_table_from(R, tr);
   } else {
+#if AT2V_TABLES_X2
     gu_cached ca1, cr1, cj;
     gu_cached_identity(cj);
     ta.store(0, cj);
@@ -139,6 +161,10 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
       gu_p3_to_cached(cj, PR);
       tr.store(j, cj);
     }
+#else
+    build_a_table_from(A, ta);
+    build_a_table_from(R, tr);
+#endif
   }
   AT2V_PHASE(3);
   pace.mark(4);
@@ -391,20 +417,7 @@ template <class TabP>
 AT2V_HD AT2V_INLINE int build_a_table(const uint32_t Aw[8], TabP& ta) {
   gu_p3 A;
   const int ok = gu_frombytes(A, Aw);
-  gu_cached ca1, cj;
-  gu_cached_identity(cj);
-  ta.store(0, cj);
-  gu_p3_to_cached(ca1, A);
-  ta.store(1, ca1);
-  gu_p3 PA = A;
-#pragma unroll 1
-  for (int j = 2; j <= 8; ++j) {
-    gu_p1p1 sa;
-    gu_add(sa, PA, ca1);
-    gu_p1p1_to_p3(PA, sa);
-    gu_p3_to_cached(cj, PA);
-    ta.store(j, cj);
-  }
+  build_a_table_from(A, ta);
   return ok;
 }
 
