@@ -13,11 +13,12 @@
 
 namespace at2v {
 
-// AT2V_GU_X2 = 1: the group law's independent products run as interleaved pairs (two MAD chains in one asm block);
-// 0: one product at a time through the single-product variants (same columns; the pair's one-MAD wraps become the single
-// functions' own wraps, always valid) — fewer live registers at the price of less ILP (A/B, profiles/r03q).
+// AT2V_GU_X2 = 1: the group law's independent products run as interleaved pairs (two MAD chains in one asm block, round
+// 2); 0 (default since round 3): one product at a time through the single-product variants (same columns; a pair's
+// one-MAD wraps become the single functions' own wraps, always valid): fewer live registers, +0.4% in two A/B runs
+// (profiles/r03r, r03s).
 #ifndef AT2V_GU_X2
-#define AT2V_GU_X2 1
+#define AT2V_GU_X2 0
 #endif
 #if AT2V_GU_X2
 #define GU_MUL_WN(a, f0, g0, b, f1, g1) fu_mul_wn(a, f0, g0, b, f1, g1)
