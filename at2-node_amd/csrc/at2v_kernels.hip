@@ -719,6 +719,51 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
   }
 }
 
+// The message reader of one record (verify_chunks' MsgSplit: the fast form when the wave's messages all end 8 bytes
+// before the buffer end), handed to body(msgword). A plain function, so the comb path below inlines it (as lambdas the
+// compiler outlined these bodies into calls).
+template <class Body>
+__device__ AT2V_INLINE int with_msg_reader(const uint8_t* __restrict__ msg, uint32_t msg_total, uint32_t b0, uint32_t bl,
+                                           Body&& body) {
+  const int msg_fast = __builtin_amdgcn_readfirstlane(__all((uint64_t)b0 + bl + 8 <= (uint64_t)msg_total) ? 1 : 0);
+  const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (b0 >> 2);
+  const uint32_t msh = (b0 & 3u) * 8;
+  auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
+  auto msg_guarded = [=](uint32_t j) -> uint32_t {
+    const uint32_t a = b0 + 4 * j;
+    const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
+    const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
+    if (sh == 0) return lo;
+    const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+  };
+  auto touched = [] {};
+  MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> msgword{msg_fast, msg_unguarded,
+                                                                                      msg_guarded, touched};
+  return body(msgword);
+}
+
+// R' of record i (clamped to the batch) from its key's comb; returns the checks that need no point arithmetic
+__device__ AT2V_INLINE int comb2_point(gu_p3& P, uint32_t i, uint32_t n, const uint8_t* __restrict__ pk,
+                                       const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+                                       uint32_t msg_total, const uint32_t* __restrict__ off, int policy, int a_ok,
+                                       const int4* __restrict__ comb_key, const DevBComb& tbc, int4* sa, int4* sr,
+                                       int lane) {
+  const uint32_t ii = i < n ? i : n - 1;
+  uint32_t Rw[8], Sw[8], Aw[8];
+  load8(Rw, sig + (size_t)ii * 64);
+  load8(Sw, sig + (size_t)ii * 64 + 32);
+  load8(Aw, pk + (size_t)ii * 32);
+  const uint32_t o0 = off[ii], len = off[ii + 1] - o0;
+  const int ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
+  const DevComb tc{comb_key, {sa, sr}, lane};
+  with_msg_reader(msg, msg_total, o0, len, [&](auto& mwd) {
+    comb_point(P, Rw, Aw, Sw, len, mwd, tc, tbc);
+    return 0;
+  });
+  return ok;
+}
+
 // Comb throughput path with two records per lane (at2v_opts.sender_comb): a chunk is 128 records, lane l
 // verifies records 128c + l and 128c + 64 + l. If all 128 hit the cache, both R' come from comb additions and their two
 // inversions share one (Montgomery's trick: 1/Z0 = Z1 / (Z0 Z1), 1/Z1 = Z0 / (Z0 Z1)); otherwise each 64-record half runs
@@ -749,107 +794,67 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
                                             : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
   for (uint32_t c = c_first; c < nchunks;) {
-    uint32_t Rw[2][8], Sw[2][8], Aw[2][8], o0[2], len[2];
-    int a_ok[2], cidx[2], hit = 1;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t i = c * 128 + 64 * h + lane;
-      const uint32_t ii = i < n ? i : n - 1;
-      load8(Rw[h], sig + (size_t)ii * 64);
-      load8(Sw[h], sig + (size_t)ii * 64 + 32);
-      load8(Aw[h], pk + (size_t)ii * 32);
-      o0[h] = off[ii];
-      len[h] = off[ii + 1] - o0[h];
-      hit &= cache_hit(cache, slot_of[ii], Aw[h], a_ok[h], cidx[h]) ? 1 : 0;
+    // the cache check of both halves keeps only each record's hit, A-decode verdict and comb index; the records' words
+    // are re-read where they are used, so at most one record's words and the other's R' are live at a time
+    const uint32_t i0 = c * 128 + lane, i1 = i0 + 64;
+    int a_ok0, a_ok1, cidx0, cidx1;
+    int hit;
+    {
+      uint32_t Aw[8];
+      load8(Aw, pk + (size_t)(i0 < n ? i0 : n - 1) * 32);
+      hit = cache_hit(cache, slot_of[i0 < n ? i0 : n - 1], Aw, a_ok0, cidx0) ? 1 : 0;
+      load8(Aw, pk + (size_t)(i1 < n ? i1 : n - 1) * 32);
+      hit &= cache_hit(cache, slot_of[i1 < n ? i1 : n - 1], Aw, a_ok1, cidx1) ? 1 : 0;
     }
     const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
     if (lane == 0) {
       atomicAdd(cache_ctl + kCtlChunks, 2ull);
       if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 2ull);
     }
-    // message reader of half h (the fast form when the wave's messages all end 8 bytes before the buffer end)
-    auto run = [&](int h, auto&& body) -> int {
-      const uint32_t b0 = o0[h], bl = len[h];
-      const int msg_fast =
-          __builtin_amdgcn_readfirstlane(__all((uint64_t)b0 + bl + 8 <= (uint64_t)msg_total) ? 1 : 0);
-      const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (b0 >> 2);
-      const uint32_t msh = (b0 & 3u) * 8;
-      auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
-      auto msg_guarded = [=](uint32_t j) -> uint32_t {
-        const uint32_t a = b0 + 4 * j;
-        const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
-        const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
-        if (sh == 0) return lo;
-        const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
-        return __builtin_amdgcn_alignbit(hi, lo, sh);
-      };
-      auto touched = [] {};
-      MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> msgword{msg_fast, msg_unguarded,
-                                                                                          msg_guarded, touched};
-      return body(msgword);
-    };
-    int good[2];
+    int good0, good1;
     if (all_hit) {
       gu_p3 P0, P1;
-      run(0, [&](auto& mwd) {
-        const DevComb tc{comb + (size_t)cidx[0] * (kCombBytes / 16), {sa, sr}, lane};
-        comb_point(P0, Rw[0], Aw[0], Sw[0], len[0], mwd, tc, tbc);
-        return 0;
-      });
-      run(1, [&](auto& mwd) {
-        const DevComb tc{comb + (size_t)cidx[1] * (kCombBytes / 16), {sa, sr}, lane};
-        comb_point(P1, Rw[1], Aw[1], Sw[1], len[1], mwd, tc, tbc);
-        return 0;
-      });
+      const int ok0 = comb2_point(P0, i0, n, pk, sig, msg, msg_total, off, policy, a_ok0,
+                                  comb + (size_t)cidx0 * (kCombBytes / 16), tbc, sa, sr, lane);
+      const int ok1 = comb2_point(P1, i1, n, pk, sig, msg, msg_total, off, policy, a_ok1,
+                                  comb + (size_t)cidx1 * (kCombBytes / 16), tbc, sa, sr, lane);
       fu zz, inv, zi;
       fu_mulc(zz, P0.Z, P1.Z);
       fu_invert(inv, zz);
+      uint32_t Rw[8];
+      load8(Rw, sig + (size_t)(i0 < n ? i0 : n - 1) * 64);
       fu_mulc(zi, inv, P1.Z);
-      good[0] = comb_prechecks(Rw[0], Aw[0], Sw[0], policy, a_ok[0]) & gu_encode_eq_zi(P0, zi, Rw[0]);
+      good0 = ok0 & gu_encode_eq_zi(P0, zi, Rw);
+      load8(Rw, sig + (size_t)(i1 < n ? i1 : n - 1) * 64);
       fu_mulc(zi, inv, P0.Z);
-      good[1] = comb_prechecks(Rw[1], Aw[1], Sw[1], policy, a_ok[1]) & gu_encode_eq_zi(P1, zi, Rw[1]);
+      good1 = ok1 & gu_encode_eq_zi(P1, zi, Rw);
     } else {
-      // one half at a time through ONE inlined copy of the ladder: the half's words are selected into plain arrays
-      // (a runtime index into Rw[2][8] would put the arrays in scratch)
+      // one half at a time through ONE inlined copy of the ladder
+      int g[2] = {0, 0};
 #pragma unroll 1
       for (int h = 0; h < 2; ++h) {
-        uint32_t R1[8], A1[8], S1[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          R1[q] = h ? Rw[1][q] : Rw[0][q];
-          A1[q] = h ? Aw[1][q] : Aw[0][q];
-          S1[q] = h ? Sw[1][q] : Sw[0][q];
-        }
-        const uint32_t b0 = h ? o0[1] : o0[0], bl = h ? len[1] : len[0];
-        const int msg_fast =
-            __builtin_amdgcn_readfirstlane(__all((uint64_t)b0 + bl + 8 <= (uint64_t)msg_total) ? 1 : 0);
-        const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (b0 >> 2);
-        const uint32_t msh = (b0 & 3u) * 8;
-        auto msg_unguarded = [=](uint32_t j) -> uint32_t { return __builtin_amdgcn_alignbit(mw[j + 1], mw[j], msh); };
-        auto msg_guarded = [=](uint32_t j) -> uint32_t {
-          const uint32_t a = b0 + 4 * j;
-          const uint32_t a0 = a & ~3u, sh = (a & 3u) * 8;
-          const uint32_t lo = load_u32_guarded(msg, a0, msg_total);
-          if (sh == 0) return lo;
-          const uint32_t hi = load_u32_guarded(msg, a0 + 4, msg_total);
-          return __builtin_amdgcn_alignbit(hi, lo, sh);
-        };
-        auto touched = [] {};
-        MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> mwd{msg_fast, msg_unguarded,
-                                                                                        msg_guarded, touched};
-        const int g = verify_half_fu(R1, A1, S1, bl, mwd, policy, ta, tr, tb0, tb1, wmax);
-        if (h) good[1] = g;
-        else good[0] = g;
+        const uint32_t ii = h ? (i1 < n ? i1 : n - 1) : (i0 < n ? i0 : n - 1);
+        uint32_t Rw[8], Sw[8], Aw[8];
+        load8(Rw, sig + (size_t)ii * 64);
+        load8(Sw, sig + (size_t)ii * 64 + 32);
+        load8(Aw, pk + (size_t)ii * 32);
+        const uint32_t o0 = off[ii], len = off[ii + 1] - o0;
+        const int gh = with_msg_reader(msg, msg_total, o0, len, [&](auto& mwd) {
+          return verify_half_fu(Rw, Aw, Sw, len, mwd, policy, ta, tr, tb0, tb1, wmax);
+        });
+        if (h) g[1] = gh;
+        else g[0] = gh;
       }
+      good0 = g[0];
+      good1 = g[1];
     }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint64_t mask = __ballot(good[h] & (c * 128 + 64 * h + lane < n));
-      const uint32_t w0 = 4 * c + 2 * h;
-      if (lane == 0) {
-        if (w0 < nwords) verdicts[w0] = (uint32_t)mask;
-        if (w0 + 1 < nwords) verdicts[w0 + 1] = (uint32_t)(mask >> 32);
-      }
+    const uint64_t m0 = __ballot(good0 & (i0 < n)), m1 = __ballot(good1 & (i1 < n));
+    if (lane == 0) {
+      const uint32_t w0 = 4 * c;
+      if (w0 < nwords) verdicts[w0] = (uint32_t)m0;
+      if (w0 + 1 < nwords) verdicts[w0 + 1] = (uint32_t)(m0 >> 32);
+      if (w0 + 2 < nwords) verdicts[w0 + 2] = (uint32_t)m1;
+      if (w0 + 3 < nwords) verdicts[w0 + 3] = (uint32_t)(m1 >> 32);
     }
     uint32_t ticket = 0;
     if (lane == 0) ticket = atomicAdd(chunk_queue, 1u);

@@ -30,6 +30,14 @@ namespace at2v {
 #ifndef AT2V_TABLES_X2
 #define AT2V_TABLES_X2 0
 #endif
+// AT2V_TABLES_EARLY = 1: each point's table is built right after its decode, so no decoded point is live across SHA-512
+// and the lattice reduction (80 words). R's table then holds [j](+R) and the sign of c1, known only after the reduction,
+// is applied per digit in the ladder (one XOR into the entry's conditional negation). Spills 75 -> 56 VGPRs, yet 1.1%
+// slower in an A/B (profiles/r03u): not the default. 0 = both tables after the reduction, from the decoded points kept
+// live (or parked: AT2V_PARK_POINTS).
+#ifndef AT2V_TABLES_EARLY
+#define AT2V_TABLES_EARLY 0
+#endif
 
 // [j]P, j = 0..8, cached form, into tp (one table; the A/B form of the interleaved build)
 template <class TabP>
@@ -62,8 +70,20 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     ok &= !enc_small_order(Rw);
     ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
   }
-  // V2: decode A and R together; R must be canonical (y < p, not x = 0 with the sign bit)
+  // V2: decode A and R; R must be canonical (y < p, not x = 0 with the sign bit)
   gu_p3 A, R;
+#if AT2V_TABLES_EARLY
+  if (kCacheable && a_cached) {  // [j]A comes from the cache entry
+    ok &= a_cached_ok;
+  } else {
+    ok &= gu_frombytes(A, Aw);
+    build_a_table_from(A, ta);
+  }
+  ok &= gu_frombytes(R, Rw);
+  ok &= enc_y_canonical(Rw);
+  ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
+  build_a_table_from(R, tr);
+#else
   if (kCacheable && a_cached) {
     ok &= gu_frombytes(R, Rw) & a_cached_ok;
   } else {
@@ -78,7 +98,8 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   }
   ok &= enc_y_canonical(Rw);
   ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
-#if AT2V_PARK_POINTS
+#endif
+#if AT2V_PARK_POINTS && !AT2V_TABLES_EARLY
   // A and R are not used again until the tables are built (after SHA-512, the lattice reduction and the recoding), and
   // holding their 80 words through those phases is what makes the compiler spill (one scratch reload and wait per
   // word, ~50 of them at the table build). Park them in the lanes' table slots (entry 8, written last by the build)
@@ -126,6 +147,10 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
 
   // tables [j]A and [j](+-R), j = 0..8: one after the other (AT2V_TABLES_X2 = 0, the default since round 3: the pair's
   // extra live registers cost more in spills than its ILP gains, profiles/r03q), or as one interleaved pair
+#if AT2V_TABLES_EARLY
+  const int rflip = hs.c1_neg;  // [c1]R = [|c1|](-R) when c1 < 0: flips the sign of every R digit
+#else
+  const int rflip = 0;
 #if AT2V_PARK_POINTS
   if (!(kCacheable && a_cached)) ta.unpark(A);
   tr.unpark(R);
@@ -166,6 +191,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     build_a_table_from(R, tr);
 #endif
   }
+#endif  // AT2V_TABLES_EARLY
   AT2V_PHASE(3);
   pace.mark(4);
 
@@ -188,7 +214,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     gu_add(tt, R3, ca);
     gu_p1p1_to_p3(R3, tt);
     tr.load_prefetched(ca);
-    gu_cached_cneg(ca, dr < 0);
+    gu_cached_cneg(ca, (dr < 0) ^ rflip);
     gu_add(tt, R3, ca);
     gu_p1p1_to_p2(R2, tt);
   }
@@ -250,7 +276,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     gu_p1p1_to_p3(R3, tt);
     tr.load_prefetched(ca);
     if (bwin) tb1.prefetch(e1 < 0 ? -e1 : e1);  // into R's stage
-    gu_cached_cneg(ca, dr < 0);
+    gu_cached_cneg(ca, (dr < 0) ^ rflip);
     gu_add(tt, R3, ca);
     if (bwin) {
       gu_p1p1_to_p3(R3, tt);

@@ -93,7 +93,8 @@ def queue_host():
         subprocess.run(["g++", "-O1" if flags else "-O2", "-g", "-std=c++17", "-pthread", *flags,
                         "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"),
                         os.path.join(ROOT, "tests", "host", "queue_host.cpp"), "-L" + oracle_dir, "-loracle",
-                        "-Wl,-rpath," + oracle_dir, "-o", exe], check=True)
+                        "-Wl,-rpath," + oracle_dir, "-o", f"{exe}.{os.getpid()}"], check=True)
+        os.replace(f"{exe}.{os.getpid()}", exe)  # atomic: parallel workers (pytest -n) never run a half-written file
         exes[kind] = exe
     return exes
 
