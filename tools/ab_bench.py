@@ -14,15 +14,21 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import at2v  # noqa: E402
 
 
-def open_lib(path):
+class Opts(ctypes.Structure):  # include/at2v.h at2v_opts (ABI v4)
+    _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int),
+                ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32), ("sender_comb", ctypes.c_uint32)]
+
+
+def open_lib(path, comb=False):
     lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
     P = ctypes.c_void_p
     lib.at2v_create.argtypes = [P, ctypes.POINTER(P)]
     lib.at2v_verify_batch_device.argtypes = [P, P, P, P, ctypes.c_size_t, P, ctypes.c_size_t, P, P]
-    lib.at2v_gen_records_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
-                                            P, P, P, P, P]
+    lib.at2v_gen_records_senders_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
+                                                    ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P]
     h = P()
-    assert lib.at2v_create(None, ctypes.byref(h)) == 0
+    o = Opts(0, 1, 0, 0, 1024 if comb else 0, 1 if comb else 0)
+    assert lib.at2v_create(ctypes.byref(o), ctypes.byref(h)) == 0
     return lib, h
 
 
@@ -33,10 +39,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--msg-len", type=int, default=100)
     ap.add_argument("--no-check", action="store_true", help="perf-only experiment builds: skip the verdict check")
+    ap.add_argument("--senders", type=int, default=0, help="records signed by this many repeating senders (0 = distinct)")
+    ap.add_argument("--comb", action="store_true", help="contexts with sender_cache 1024 + sender_comb (AT2 traffic)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L = a.n, a.msg_len
-    libs = [open_lib(p) for p in a.libs]
+    libs = [open_lib(p, a.comb) for p in a.libs]
     s = torch.cuda.current_stream()
     d_pk = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_sig = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
@@ -44,8 +52,8 @@ def main():
     d_off = torch.empty(n + 1, dtype=torch.int32, device="cuda")
     d_ver = torch.zeros((n + 31) // 32, dtype=torch.int32, device="cuda")
     lib0, h0 = libs[0]
-    assert lib0.at2v_gen_records_device(h0, 0x4154325F, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
-                                        d_off.data_ptr(), s.cuda_stream) == 0
+    assert lib0.at2v_gen_records_senders_device(h0, 0x4154325F, 0, n, L, a.senders, d_pk.data_ptr(), d_sig.data_ptr(),
+                                                d_msg.data_ptr(), d_off.data_ptr(), s.cuda_stream) == 0
     torch.cuda.synchronize()
     times = {p: [] for p in a.libs}
     for r in range(a.rounds + 1):
