@@ -13,26 +13,32 @@ SRC = os.path.join(ROOT, "tests", "host", "verify_host.cpp")
 EXE = os.path.join(ROOT, "tests", "host", "verify_host")
 
 
-def _build(cmd, exe):
-    """compile to a per-process name, then rename into place: parallel test workers (pytest -n) never execute a file
-    another worker is still writing"""
-    tmp = f"{exe}.{os.getpid()}"
-    subprocess.run(cmd + ["-o", tmp], check=True)
-    os.replace(tmp, exe)
-    return exe
+INC = "-I" + os.path.join(ROOT, "at2-node_amd", "csrc")
+BUILDS = {  # the plain build and the sanitized one (-O0: the always-inline field code takes minutes at -O1 under ASan)
+    EXE: ["g++", "-O2", "-std=c++17", INC, SRC],
+    EXE + "_asan": ["g++", "-O0", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all", INC, SRC],
+}
 
 
 @pytest.fixture(scope="module")
-def host_exe():
-    return _build(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC], EXE)
+def host_exes():
+    """both builds, compiled CONCURRENTLY (each takes ~2.5 min), each to a per-process name and then renamed into place,
+    so parallel test workers (pytest -n) never execute a file another worker is still writing"""
+    procs = {exe: subprocess.Popen(cmd + ["-o", f"{exe}.{os.getpid()}"]) for exe, cmd in BUILDS.items()}
+    for exe, pr in procs.items():
+        assert pr.wait() == 0, f"build of {exe} failed"
+        os.replace(f"{exe}.{os.getpid()}", exe)
+    return list(BUILDS)
 
 
 @pytest.fixture(scope="module")
-def host_exe_asan():
-    exe = EXE + "_asan"
-    # -O0: the always-inline field code takes minutes to compile at -O1 under the sanitizers
-    return _build(["g++", "-O0", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-                   "-I" + os.path.join(ROOT, "at2-node_amd", "csrc"), SRC], exe)
+def host_exe(host_exes):
+    return host_exes[0]
+
+
+@pytest.fixture(scope="module")
+def host_exe_asan(host_exes):
+    return host_exes[1]
 
 
 MODES = [0, 1, 2, 3, 4, 5]
