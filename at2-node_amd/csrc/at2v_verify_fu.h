@@ -73,16 +73,18 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   // V2: decode A and R; R must be canonical (y < p, not x = 0 with the sign bit)
   gu_p3 A, R;
 #if AT2V_TABLES_EARLY
+  // 1: both tables early; 2: A's table early, R kept live (its table after the reduction); 3: R's table early (sign of
+  // c1 per digit), A kept live
   if (kCacheable && a_cached) {  // [j]A comes from the cache entry
     ok &= a_cached_ok;
   } else {
     ok &= gu_frombytes(A, Aw);
-    build_a_table_from(A, ta);
+    if (AT2V_TABLES_EARLY != 3) build_a_table_from(A, ta);
   }
   ok &= gu_frombytes(R, Rw);
   ok &= enc_y_canonical(Rw);
   ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
-  build_a_table_from(R, tr);
+  if (AT2V_TABLES_EARLY != 2) build_a_table_from(R, tr);
 #else
   if (kCacheable && a_cached) {
     ok &= gu_frombytes(R, Rw) & a_cached_ok;
@@ -148,7 +150,17 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   // tables [j]A and [j](+-R), j = 0..8: one after the other (AT2V_TABLES_X2 = 0, the default since round 3: the pair's
   // extra live registers cost more in spills than its ILP gains, profiles/r03q), or as one interleaved pair
 #if AT2V_TABLES_EARLY
-  const int rflip = hs.c1_neg;  // [c1]R = [|c1|](-R) when c1 < 0: flips the sign of every R digit
+  const int rflip = AT2V_TABLES_EARLY != 2 ? hs.c1_neg : 0;  // [c1]R = [|c1|](-R) when c1 < 0: flips every R digit
+  if (AT2V_TABLES_EARLY == 2) {
+    if (hs.c1_neg) {
+      fu_neg(R.X, R.X, FU_KC);
+      fu_carry(R.X);
+      fu_neg(R.T, R.T, FU_KC);
+      fu_carry(R.T);
+    }
+    build_a_table_from(R, tr);
+  }
+  if (AT2V_TABLES_EARLY == 3 && !(kCacheable && a_cached)) build_a_table_from(A, ta);
 #else
   const int rflip = 0;
 #if AT2V_PARK_POINTS
