@@ -1,23 +1,24 @@
 // at2v_comb.h — verify from per-key comb tables (at2v_opts.sender_comb).
 //
 // AT2 senders issue consecutive sequences (/root/reference/src/bin/server/accounts/account.rs:36-43): one public key A
-// signs many payloads. For such a key the device keeps a comb of -A, C[i][j] = [j 2^(8i)](-A) for i = 0..31, j = 0..128
+// signs many payloads. For such a key the device keeps a comb of -A, C[i][j] = [j 2^(10i)](-A) for i = 0..25, j = 0..512
 // (cached form), next to the context's comb of B, D[i][j] = [j 2^(16i)]B for i = 0..15, j = 0..2^15 (affine Niels).
-// Then dalek's point R' = [k](-A) + [s]B is a sum of 32 + 16 table entries, no doublings:
-//   k = sum_i e_i 2^(8i), e_i in [-128, 127] (sc_recode8)   ->  [k](-A) = sum_i +-C[i][|e_i|]
+// Then dalek's point R' = [k](-A) + [s]B is a sum of 26 + 16 table entries, no doublings:
+//   k = sum_i e_i 2^(10i), e_i in [-512, 511] (sc_recode_w) ->  [k](-A) = sum_i +-C[i][|e_i|]
 //   s = sum_i f_i 2^(16i), f_i in [-2^15, 2^15) (sc_recode16) ->  [s]B   = sum_i +-D[i][|f_i|]
 // and the verdict is dalek's own comparison, enc(R') == R_bytes (the full-length form, DESIGN.md §4: no lattice
 // reduction, no decode of R). Any correct evaluation of [k](-A) + [s]B is the same group element, so the verdicts are
 // those of the ladder kernels (and of the oracle), for every key the comb was built from, small-order and mixed-order
 // keys included; a key that fails dalek's decode has verdict 0 whatever the comb holds.
 //
-// Cost per verify: 32 additions with cached entries (8 M) + 16 mixed additions (7 M) + one inversion (254 S + 11 M) +
-// SHA-512, against the half-size ladder's 2 exponentiations + 2 tables + 33 windows: ~3.5x fewer
-// multiplications. The comb of one key is 32 x 129 x 160 B = 660 KB, built once (comb_build_lane).
+// Cost per verify: 26 additions with cached entries (8 M) + 16 mixed additions (7 M) + one inversion (254 S + 11 M; shared
+// by two records in the throughput kernel) + SHA-512, against the half-size ladder's 2 exponentiations + 2 tables + 33
+// windows: ~4x fewer multiplications. The comb of one key is 26 x 513 x 160 B = 2.1 MB (10-bit windows),
+// built once (comb_build_lane).
 //   TabC  : prefetch(stage, i, j) / load_prefetched(stage, gu_cached&)   entry C[i][j] of this lane's key
 //   TabBC : prefetch(stage, i, j) / load_prefetched(stage, gu_niels&)    entry D[i][j]
 // Two stages alternate: the entry of the next addition is fetched while this one is computed. The low-latency kernel
-// splits one record's work over four waves (decode R | 16 B entries | SHA-512 + 16 A entries | SHA-512 + 16 A entries)
+// splits one record's work over four waves (decode R | 16 B entries | SHA-512 + 13 A entries | SHA-512 + 13 A entries)
 // and compares R' with the decoded R projectively (comb_check_split).
 #pragma once
 #include "at2v_gu.h"
@@ -25,12 +26,23 @@
 
 namespace at2v {
 
-constexpr int kCombPos = 32;          // A comb positions (radix 2^8)
-constexpr int kCombEntries = 129;     // j = 0..128 per position (j = 0: the identity)
+// A comb window: signed radix-2^w digits of k (w = AT2V_COMB_BITS). w = 10 (default): 26 positions x 513 entries, 2.1 MB
+// per key; w = 8: 32 positions x 129 entries, 660 KB per key, 6 additions more per verify (368.4 vs 399.9 M/s on 64-sender
+// traffic, profiles/r03z).
+#ifndef AT2V_COMB_BITS
+#define AT2V_COMB_BITS 10
+#endif
+constexpr int kCombBits = AT2V_COMB_BITS;
+static_assert(kCombBits >= 4 && kCombBits <= 15, "A comb window");
+constexpr int kCombPos = (254 + kCombBits - 1) / kCombBits;    // positions (sc_recode_w's digit count)
+constexpr int kCombEntries = (1 << (kCombBits - 1)) + 1;        // j = 0..2^(w-1) per position (j = 0: the identity)
+constexpr int kCombHalf = 1 << (kCombBits - 2);                 // entries one builder lane makes
+constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
+static_assert(2 * kCombPos <= 64, "one builder lane per position and half");
 constexpr int kBCombPos = 16;         // B comb positions (radix 2^16)
 constexpr int kBCombEntries = 32769;  // j = 0..2^15
 constexpr int kCombGranules = 10;     // cached point: 40 words
-constexpr size_t kCombBytes = (size_t)kCombPos * kCombEntries * kCombGranules * 16;  // 660,480 B per key
+constexpr size_t kCombBytes = (size_t)kCombPos * kCombEntries * kCombGranules * 16;  // per key
 
 // R' (p2) encoded as dalek's CompressedEdwardsY (y canonical, sign bit = low bit of canonical x) == R_bytes
 AT2V_HD AT2V_INLINE int gu_encode_eq(const gu_p2& P, const uint32_t Rw[8]) {
@@ -75,10 +87,10 @@ AT2V_HD AT2V_INLINE int comb_prechecks(const uint32_t Rw[8], const uint32_t Aw[8
   return ok;
 }
 
-// V3 and the recoding of k: kd = signed radix-256 digits of SHA-512(R || A || M) mod l
+// V3 and the recoding of k: kd = signed radix-2^w digits of SHA-512(R || A || M) mod l, e_i + 2^(w-1) in 16-bit fields
 template <class MsgWord>
-AT2V_HD AT2V_INLINE void comb_k_digits(uint32_t kd[8], const uint32_t Rw[8], const uint32_t Aw[8], uint32_t len,
-                                       MsgWord msgword) {
+AT2V_HD AT2V_INLINE void comb_k_digits(uint32_t kd[kCombDigitWords], const uint32_t Rw[8], const uint32_t Aw[8],
+                                       uint32_t len, MsgWord msgword) {
   uint32_t k[8];
   uint32_t pre[16];
 #pragma unroll
@@ -91,18 +103,22 @@ AT2V_HD AT2V_INLINE void comb_k_digits(uint32_t kd[8], const uint32_t Rw[8], con
   uint32_t hw[16];
   sha512_digest_words(hw, h);
   sc_reduce512(k, hw);
-  sc_recode8(kd, k);
+  uint32_t d[kCombPos];
+  sc_recode_w<kCombBits>(d, k);
+#pragma unroll
+  for (int q = 0; q < kCombDigitWords; ++q)
+    kd[q] = d[2 * q] | (2 * q + 1 < kCombPos ? d[2 * q + 1] << 16 : 0u);
 }
 
-AT2V_HD AT2V_INLINE int comb_adigit(const uint32_t kd[8], int i) {
-  return (int)((sel8(kd, i >> 2) >> (8 * (i & 3))) & 255) - 128;
+AT2V_HD AT2V_INLINE int comb_adigit(const uint32_t kd[kCombDigitWords], int i) {
+  return (int)((seln<kCombDigitWords>(kd, i >> 1) >> (16 * (i & 1))) & 0xffff) - (1 << (kCombBits - 1));
 }
 AT2V_HD AT2V_INLINE int comb_bdigit(const uint32_t sd[8], int i) {
   return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000;
 }
 
 // acc += sum over positions i in [i0, i1) of the signed entry C[i][e_i] (A comb, cached form, kAComb) or D[i][f_i] (B
-// comb, affine Niels). i1 - i0 even; the entry of addition m + 1 is fetched (into the other stage) while m is computed.
+// comb, affine Niels). The entry of addition m + 1 is fetched (into the other stage) while m is computed.
 template <bool kAComb, class Tab>
 AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int i1, const Tab& tab) {
   auto digit = [&](int i) {
@@ -117,6 +133,7 @@ AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // stage h holds entry i + h
       const int m = i + h;
+      if (m >= i1) break;  // an odd count (wave-uniform)
       const int en = m + 1 < i1 ? digit(m + 1) : 0;
       if constexpr (kAComb) {
         gu_cached ca;
@@ -141,7 +158,7 @@ AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int
 template <class TabC, class TabBC, class MsgWord>
 AT2V_HD AT2V_INLINE void comb_point(gu_p3& acc, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
                                     uint32_t len, MsgWord msgword, const TabC& tc, const TabBC& tb) {
-  uint32_t kd[8], sd[8];
+  uint32_t kd[kCombDigitWords], sd[8];
   comb_k_digits(kd, Rw, Aw, len, msgword);
   sc_recode16(sd, Sw);
   gu_p3_identity(acc);
@@ -154,7 +171,7 @@ template <class TabC, class TabBC, class MsgWord>
 AT2V_HD AT2V_INLINE int verify_comb_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                        MsgWord msgword, int policy, int a_ok, const TabC& tc, const TabBC& tb) {
   const int ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
-  uint32_t kd[8], sd[8];
+  uint32_t kd[kCombDigitWords], sd[8];
   comb_k_digits(kd, Rw, Aw, len, msgword);
   sc_recode16(sd, Sw);
   AT2V_PHASE(2);
@@ -201,9 +218,10 @@ AT2V_HD AT2V_INLINE int comb_check_split(const gu_p3& R, const gu_p3& Pa0, const
   return ex & fu_iszero(d);
 }
 
-// One lane's share of the comb of key A: position pos (0..31), half h (0..1) -> entries j = 64h + 1 .. 64h + 64 of
-// C[pos][j] = [j 2^(8 pos)](-A), cached form, through store(j, const gu_cached&); the h = 0 lane also stores j = 0 (the
-// identity). 64 lanes (pos = lane >> 1, h = lane & 1) build the whole comb. Every lane decodes A (dalek rules) and
+// One lane's share of the comb of key A: position pos (0..kCombPos-1), half h (0..1) -> entries
+// j = kCombHalf h + 1 .. kCombHalf (h + 1) of C[pos][j] = [j 2^(w pos)](-A), cached form, through
+// store(j, const gu_cached&); the h = 0 lane also stores j = 0 (the identity). 2 kCombPos lanes (pos = lane >> 1,
+// h = lane & 1) build the whole comb; a lane with pos >= kCombPos stores nothing. Every lane decodes A (dalek rules) and
 // returns the decode verdict; an undecodable A yields a comb that no verdict depends on.
 template <class Store>
 AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, Store&& store) {
@@ -213,7 +231,8 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
   fu_carry(P.X);
   fu_neg(P.T, P.T, FU_KC);
   fu_carry(P.T);
-  // Pi = [2^(8 pos)](-A): every lane runs the 31 x 8 doublings and keeps its position's point
+  if (pos >= kCombPos) return ok;
+  // Pi = [2^(w pos)](-A): every lane runs the (kCombPos - 1) x w doublings and keeps its position's point
   gu_p3 Pi = P, Q = P;
   gu_p2 Q2;
   gu_p1p1 t;
@@ -221,7 +240,7 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
   for (int r = 1; r < kCombPos; ++r) {
     gu_p3_to_p2(Q2, Q);
 #pragma unroll 1
-    for (int d = 0; d < 7; ++d) {
+    for (int d = 0; d < kCombBits - 1; ++d) {
       gu_p2_dbl(t, Q2);
       gu_p1p1_to_p2(Q2, t);
     }
@@ -231,13 +250,13 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
   }
   gu_cached c1;
   gu_p3_to_cached(c1, Pi);
-  // first multiple of this half: [1]Pi (h = 0) or [65]Pi = [64]Pi + Pi (h = 1)
+  // first multiple of this half: [1]Pi (h = 0) or [kCombHalf + 1]Pi = [2^(w-2)]Pi + Pi (h = 1)
   gu_p3 S = Pi;
   {
     gu_p2 D2;
     gu_p3_to_p2(D2, Pi);
 #pragma unroll 1
-    for (int d = 0; d < 5; ++d) {
+    for (int d = 0; d < kCombBits - 3; ++d) {
       gu_p2_dbl(t, D2);
       gu_p1p1_to_p2(D2, t);
     }
@@ -256,10 +275,10 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
   }
   gu_cached cj;
 #pragma unroll 1
-  for (int m = 0; m < 64; ++m) {
+  for (int m = 0; m < kCombHalf; ++m) {
     gu_p3_to_cached(cj, S);
-    store(64 * h + 1 + m, cj);
-    if (m + 1 < 64) {
+    store(kCombHalf * h + 1 + m, cj);
+    if (m + 1 < kCombHalf) {
       gu_add(t, S, c1);
       gu_p1p1_to_p3(S, t);
     }

@@ -674,7 +674,7 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
           const DevBComb tb{bcomb, {st0, st1}, lane};
           comb_sum<false>(P, sd, 0, kBCombPos, tb);
         } else {
-          uint32_t kd[8];
+          uint32_t kd[kCombDigitWords];
           comb_k_digits(kd, Rw, Aw, len, msgword);
           const DevComb tc{comb + (size_t)comb_idx * (kCombBytes / 16), {st0, st1}, lane};
           comb_sum<true>(P, kd, w == 2 ? 0 : kCombPos / 2, w == 2 ? kCombPos / 2 : kCombPos, tc);

@@ -51,9 +51,9 @@ typedef struct {
                                public keys, 0 = off. When full it is cleared and refilled. A record whose sender A is cached skips decoding A and building
                                its [j]A table; the verdict is unchanged (the cache holds only values derived from the
                                32 bytes of A, and every hit is confirmed by comparing those bytes). */
-  uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(8i)](-A), 660 KB
-                               per key, sender_cache x 660 KB per device, plus a 67 MB comb of B per context), and a
-                               64-record chunk whose senders are all cached is verified by 48 table additions and one
+  uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(10i)](-A), 2.1 MB
+                               per key, sender_cache x 2.1 MB per device, plus a 67 MB comb of B per context), and a
+                               64-record chunk whose senders are all cached is verified by 42 table additions and one
                                inversion instead of the doubling ladder (~3x fewer multiplications; launches of any size,
                                small batches included). Same verdicts. 0 = off. */
 } at2v_opts;

@@ -111,7 +111,7 @@ struct HostComb {
   int a_ok = 0;
   mutable int pend[2] = {0, 0};
   explicit HostComb(const uint32_t A[8]) : e((size_t)kCombPos * kCombEntries) {
-    for (int lane = 0; lane < 64; ++lane) {
+    for (int lane = 0; lane < 2 * kCombPos; ++lane) {
       const int pos = lane >> 1;
       a_ok = comb_build_lane(A, pos, lane & 1,
                              [&](int j, const gu_cached& c) { e[(size_t)pos * kCombEntries + j] = c; });
@@ -193,7 +193,7 @@ int main(int argc, char** argv) {
       auto split = [&](int policy) {
         gu_p3 Rp, Pb, Pa0, Pa1;
         const int ok0 = comb_decode_r(Rp, R) & comb_prechecks(R, A, S, policy, c.a_ok);
-        uint32_t sd[8], kd[8];
+        uint32_t sd[8], kd[kCombDigitWords];
         sc_recode16(sd, S);
         gu_p3_identity(Pb);
         comb_sum<false>(Pb, sd, 0, kBCombPos, bcomb);

@@ -74,7 +74,8 @@ def test_config1_traffic_every_chunk_hits(at2v_mod, oracle, comb):
 def test_golden_sets_with_cache(at2v_mod, golden, policy, comb):
     """every golden fixture set, twice (cold, then warm cache), both policies: the small-order, non-canonical and
     off-curve senders of the adversarial/edge sets are cached with their decode verdicts"""
-    with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 15, sender_comb=comb) as v:
+    # 16,384 keys hold every set's senders (<= 9,200 distinct); with combs that is 16,384 x 2.1 MB = 35 GB of HBM
+    with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 14, sender_comb=comb) as v:
         for name in golden_io.SETS:
             g = golden[name]
             want = g.dalek if policy == "dalek" else g.sodium
