@@ -7,6 +7,8 @@ For batches of B records (default 1, 20, 64, 1024), each measured `--reps` times
   sync     : wall time of at2v_verify_batch (host arrays: H2D, kernel, D2H, synchronise);
   queue    : wall time from at2v_queue_submit of the B records to the last verdict polled (eager queue, idle,
              one batch in flight at a time);
+  first    : (--comb 1) device time of the FIRST launch of the B records in a fresh context, whose B keys are new:
+             the cache lookup, one comb build per new key, then the verify (the cost a first-seen sender pays once);
 reports p50/p90 per stage as JSON. Records come from the oracle generator (all valid), checked once per size."""
 import argparse
 import json
@@ -55,6 +57,19 @@ def main():
         d_msg = torch.from_numpy(np.concatenate([m, np.zeros(16, np.uint8)])).cuda()
         d_off = torch.from_numpy(f.view(np.int32).copy()).cuda()
         d_ver = torch.zeros((B + 31) // 32, dtype=torch.int32, device="cuda")
+        first_us = None
+        if a.comb:
+            vc = at2v.BatchVerifier(device=0, sender_cache=1024, sender_comb=True)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            vc.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), int(f[-1]), d_off.data_ptr(),
+                                   B, d_ver.data_ptr(), s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            first_us = e0.elapsed_time(e1) * 1e3
+            assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
+            vc.close()
         kern, sync, queue = [], [], []
         for r in range(a.reps + 5):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -79,6 +94,8 @@ def main():
         assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
         out["sizes"][B] = {k: {"p50_us": pct(x, 50), "p90_us": pct(x, 90)} for k, x in
                            (("kernel", kern), ("sync", sync), ("queue", queue))}
+        if first_us is not None:
+            out["sizes"][B]["first_launch_new_keys_us"] = first_us
         print(B, json.dumps(out["sizes"][B]), file=sys.stderr)
     q.close()
     v.close()
