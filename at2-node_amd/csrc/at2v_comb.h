@@ -36,9 +36,15 @@ constexpr int kCombBits = AT2V_COMB_BITS;
 static_assert(kCombBits >= 4 && kCombBits <= 15, "A comb window");
 constexpr int kCombPos = (254 + kCombBits - 1) / kCombBits;    // positions (sc_recode_w's digit count)
 constexpr int kCombEntries = (1 << (kCombBits - 1)) + 1;        // j = 0..2^(w-1) per position (j = 0: the identity)
-constexpr int kCombHalf = 1 << (kCombBits - 2);                 // entries one builder lane makes
+// Comb builders: a launch with few new keys gives each key a 256-thread block, 8 lanes per position (kCombWideLog2: the
+// latency of a first-seen sender); one with many gives each key a wave, 2 lanes per position (kCombNarrowLog2: fewer
+// redundant position chains when the waves outnumber the SIMDs). Both build the same points (representations differ).
+constexpr int kCombWideLog2 = 3, kCombNarrowLog2 = 1;
+static_assert(kCombBits - 1 - kCombWideLog2 >= 1, "comb builder parts");
+static_assert((kCombPos << kCombWideLog2) <= 256, "one 256-thread block builds a key's comb");
+static_assert((kCombPos << kCombNarrowLog2) <= 64, "one wave builds a key's comb");
+constexpr int kCombWideMaxKeys = 256;  // new keys per launch up to which the wide builder runs (1,024 waves)
 constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
-static_assert(2 * kCombPos <= 64, "one builder lane per position and half");
 constexpr int kBCombPos = 16;         // B comb positions (radix 2^16)
 constexpr int kBCombEntries = 32769;  // j = 0..2^15
 constexpr int kCombGranules = 10;     // cached point: 40 words
@@ -218,13 +224,18 @@ AT2V_HD AT2V_INLINE int comb_check_split(const gu_p3& R, const gu_p3& Pa0, const
   return ex & fu_iszero(d);
 }
 
-// One lane's share of the comb of key A: position pos (0..kCombPos-1), half h (0..1) -> entries
-// j = kCombHalf h + 1 .. kCombHalf (h + 1) of C[pos][j] = [j 2^(w pos)](-A), cached form, through
-// store(j, const gu_cached&); the h = 0 lane also stores j = 0 (the identity). 2 kCombPos lanes (pos = lane >> 1,
-// h = lane & 1) build the whole comb; a lane with pos >= kCombPos stores nothing. Every lane decodes A (dalek rules) and
-// returns the decode verdict; an undecodable A yields a comb that no verdict depends on.
-template <class Store>
+// One lane's share of the comb of key A, with 2^kPartsLog2 lanes per position: position pos (0..kCombPos-1), part h ->
+// entries j = kPart h + 1 .. kPart (h + 1) (kPart = 2^(w-1-kPartsLog2)) of C[pos][j] = [j 2^(w pos)](-A), cached form,
+// through store(j, const gu_cached&); the h = 0 lane also stores j = 0 (the identity). kCombPos 2^kPartsLog2 lanes
+// (pos = lane >> kPartsLog2, h = the low bits) build the whole comb; a lane with pos >= kCombPos stores nothing.
+// Every lane decodes A (dalek rules) and returns the decode verdict; an undecodable A yields a comb that no verdict
+// depends on. Per lane: (kCombPos - 1) w doublings (the position chain), log2(kPart) doublings and h additions to
+// the part's first multiple, kPart additions (w = 10: 8 parts, 256 doublings and at most 71 additions; 2 parts, 258
+// doublings and at most 257 additions).
+template <int kPartsLog2, class Store>
 AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, Store&& store) {
+  constexpr int kPartBits = kCombBits - 1 - kPartsLog2;
+  constexpr int kPart = 1 << kPartBits;
   gu_p3 P;
   const int ok = gu_frombytes(P, Aw);
   fu_neg(P.X, P.X, FU_KC);  // -A
@@ -250,23 +261,26 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
   }
   gu_cached c1;
   gu_p3_to_cached(c1, Pi);
-  // first multiple of this half: [1]Pi (h = 0) or [kCombHalf + 1]Pi = [2^(w-2)]Pi + Pi (h = 1)
+  // first multiple of this part: [kPart h + 1]Pi = Pi + h [kPart]Pi
   gu_p3 S = Pi;
   {
     gu_p2 D2;
     gu_p3_to_p2(D2, Pi);
 #pragma unroll 1
-    for (int d = 0; d < kCombBits - 3; ++d) {
+    for (int d = 0; d < kPartBits - 1; ++d) {
       gu_p2_dbl(t, D2);
       gu_p1p1_to_p2(D2, t);
     }
     gu_p2_dbl(t, D2);
     gu_p3 D;
     gu_p1p1_to_p3(D, t);
-    gu_add(t, D, c1);
-    gu_p3 S65;
-    gu_p1p1_to_p3(S65, t);
-    if (h) S = S65;
+    gu_cached dc;
+    gu_p3_to_cached(dc, D);
+#pragma unroll 1
+    for (int m = 0; m < h; ++m) {
+      gu_add(t, S, dc);
+      gu_p1p1_to_p3(S, t);
+    }
   }
   if (h == 0) {
     gu_cached id;
@@ -275,10 +289,10 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
   }
   gu_cached cj;
 #pragma unroll 1
-  for (int m = 0; m < kCombHalf; ++m) {
+  for (int m = 0; m < kPart; ++m) {
     gu_p3_to_cached(cj, S);
-    store(kCombHalf * h + 1 + m, cj);
-    if (m + 1 < kCombHalf) {
+    store(kPart * h + 1 + m, cj);
+    if (m + 1 < kPart) {
       gu_add(t, S, c1);
       gu_p1p1_to_p3(S, t);
     }

@@ -1414,36 +1414,47 @@ __global__ __launch_bounds__(256) void cache_build_kernel(const uint8_t* __restr
   ent[2] = make_int4(ok, 1, (int)e.z, 0);
 }
 
-// With combs on, the whole build of a launch's claims: one wave per claim (persistent grid) writes the comb of -A at claim
-// index u (comb_build_lane, lane = position x half) and, from lane 0, the entry's key and meta (dalek's decode verdict,
-// valid, u); a claim beyond the capacity is written invalid. (One kernel instead of cache_build_kernel + this one: one
-// dependent launch less per batch, which the small-batch latency pays.)
-__global__ __launch_bounds__(256) void cache_comb_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t nw = gridDim.x * 4;
-  const unsigned long long cnt = __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < cnt; t += nw) {
-    const uint4 e = c.new_list[t];
-    int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
-    if (e.z >= c.capacity) {  // wave-uniform
-      if (lane == 0) ent[2] = make_int4(0, 0, 0, 0);
-      continue;
-    }
-    uint32_t a[8];
-    load8(a, pk + (size_t)e.y * 32);
-    int4* cb = c.comb + (size_t)e.z * (kCombBytes / 16);
-    const int pos = lane >> 1;
-    const int ok = comb_build_lane(a, pos, lane & 1, [&](int j, const gu_cached& p) {
-      const int32_t* w = reinterpret_cast<const int32_t*>(&p);
-      int4* dst = cb + ((size_t)pos * kCombEntries + j) * kCombGranules;
+// One claim of the comb build: thread g of the claim's group (2^kPartsLog2 threads per position) writes its share of the
+// comb of -A at claim index u (comb_build_lane), and g = 0 the entry's key and meta (dalek's decode verdict, valid, u); a
+// claim beyond the capacity is written invalid. The group is block- or wave-uniform.
+template <int kPartsLog2>
+__device__ AT2V_INLINE void comb_claim(const uint8_t* __restrict__ pk, const CacheArgs& c, uint32_t t, int g) {
+  const uint4 e = c.new_list[t];
+  int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
+  if (e.z >= c.capacity) {
+    if (g == 0) ent[2] = make_int4(0, 0, 0, 0);
+    return;
+  }
+  uint32_t a[8];
+  load8(a, pk + (size_t)e.y * 32);
+  int4* cb = c.comb + (size_t)e.z * (kCombBytes / 16);
+  const int pos = g >> kPartsLog2;
+  const int ok = comb_build_lane<kPartsLog2>(a, pos, g & ((1 << kPartsLog2) - 1), [&](int j, const gu_cached& p) {
+    const int32_t* w = reinterpret_cast<const int32_t*>(&p);
+    int4* dst = cb + ((size_t)pos * kCombEntries + j) * kCombGranules;
 #pragma unroll
-      for (int q = 0; q < kCombGranules; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-    });
-    if (lane == 0) {
-      ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
-      ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
-      ent[2] = make_int4(ok, 1, (int)e.z, 0);
-    }
+    for (int q = 0; q < kCombGranules; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  });
+  if (g == 0) {
+    ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
+    ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
+    ent[2] = make_int4(ok, 1, (int)e.z, 0);
+  }
+}
+
+// With combs on, the whole build of a launch's claims (persistent grid): up to kCombWideMaxKeys claims, one 256-thread
+// block per claim and 8 threads per position (the latency of a first-seen sender: 0.84-0.96 ms for 1-64 new keys,
+// profiles/r03zf); more claims, one wave per claim and 2 lanes per position (fewer redundant position chains once the
+// waves outnumber the SIMDs). (One kernel instead of cache_build_kernel + this one: one dependent launch less per batch,
+// which the small-batch latency pays.)
+__global__ __launch_bounds__(256) void cache_comb_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
+  const unsigned long long cnt = __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (cnt <= (unsigned long long)kCombWideMaxKeys) {
+    for (uint32_t t = blockIdx.x; t < cnt; t += gridDim.x) comb_claim<kCombWideLog2>(pk, c, t, (int)threadIdx.x);
+  } else {
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < cnt; t += nw)
+      comb_claim<kCombNarrowLog2>(pk, c, t, (int)(threadIdx.x & 63));
   }
 }
 
@@ -1510,9 +1521,9 @@ hipError_t launch_cache_prepare(const CacheArgs& c, const uint8_t* pk, uint32_t 
     hipLaunchKernelGGL(cache_build_kernel, dim3(blocks), dim3(256), 0, stream, pk, c);
     return hipGetLastError();
   }
-  // one wave per claim; a launch claims at most n entries (waves loop over more)
-  const uint32_t waves = n < 2048u ? n : 2048u;
-  hipLaunchKernelGGL(cache_comb_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, pk, c);
+  // a block per claim (few claims) or a wave per claim; a launch claims at most n entries (the grid loops over more)
+  const uint32_t blocks_c = n < 512u ? n : 512u;
+  hipLaunchKernelGGL(cache_comb_kernel, dim3(blocks_c), dim3(256), 0, stream, pk, c);
   return hipGetLastError();
 }
 

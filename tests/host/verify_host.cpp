@@ -105,16 +105,22 @@ struct HostTabBFu {
   void load_prefetched(gu_niels& n) const { n = t[pending]; }
 };
 
-// comb of one key (at2v_comb.h), built by the 64 lanes' comb_build_lane exactly as the device's builder does
+// comb of one key (at2v_comb.h), built by comb_build_lane over all lanes exactly as the device's builders do
 struct HostComb {
   std::vector<gu_cached> e;
   int a_ok = 0;
   mutable int pend[2] = {0, 0};
   explicit HostComb(const uint32_t A[8]) : e((size_t)kCombPos * kCombEntries) {
-    for (int lane = 0; lane < 2 * kCombPos; ++lane) {
-      const int pos = lane >> 1;
-      a_ok = comb_build_lane(A, pos, lane & 1,
-                             [&](int j, const gu_cached& c) { e[(size_t)pos * kCombEntries + j] = c; });
+    // keys alternate between the device's two builder shapes (8 and 2 lanes per position, at2v_comb.h)
+    if (A[0] & 1) build<kCombWideLog2>(A);
+    else build<kCombNarrowLog2>(A);
+  }
+  template <int kLog2>
+  void build(const uint32_t A[8]) {
+    for (int lane = 0; lane < (kCombPos << kLog2); ++lane) {
+      const int pos = lane >> kLog2;
+      a_ok = comb_build_lane<kLog2>(A, pos, lane & ((1 << kLog2) - 1),
+                                    [&](int j, const gu_cached& c) { e[(size_t)pos * kCombEntries + j] = c; });
     }
   }
   void prefetch(int st, int i, int j) const { pend[st] = i * kCombEntries + j; }
