@@ -52,7 +52,7 @@ class VerifyError(Exception):
     """Signature rejected (drop::crypto::sign::VerifyError)."""
 
 
-ABI_VERSION = 4  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
+ABI_VERSION = 5  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
 E_PEER = -7      # AT2V_E_PEER: another rank of the communicator failed this collective batch
 
 
@@ -71,7 +71,9 @@ class _Info(ctypes.Structure):
                 ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int), ("vgprs", ctypes.c_int),
                 ("rank", ctypes.c_int), ("world", ctypes.c_int), ("gathers", ctypes.c_uint64),
                 ("cache_entries", ctypes.c_uint64), ("cache_chunks", ctypes.c_uint64),
-                ("cache_chunk_hits", ctypes.c_uint64)]
+                ("cache_chunk_hits", ctypes.c_uint64), ("cache_capacity", ctypes.c_uint64),
+                ("cache_claims", ctypes.c_uint64), ("cache_evicted", ctypes.c_uint64),
+                ("cache_compactions", ctypes.c_uint64)]
 
 
 UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)

@@ -71,7 +71,7 @@ QUEUE_SENDER_COMB = 2  # include/at2v.h AT2V_QUEUE_SENDER_COMB: per-sender combs
 class _QueueOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("policy", ctypes.c_int), ("max_batch", ctypes.c_uint32),
                 ("max_delay_us", ctypes.c_uint32), ("max_msg_bytes", ctypes.c_uint32), ("depth", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32)]
 
 
 class _QueueStats(ctypes.Structure):
@@ -142,13 +142,14 @@ class IngestQueue:
     """GPU-backed batching queue: submit records, poll (ticket, verdict) in submission order."""
 
     def __init__(self, device: int = 0, policy="dalek", max_batch: int = 65536, max_delay_us: int = 1000,
-                 max_msg_bytes: int = 256, depth: int = 3, eager: bool = False, sender_comb: bool = False):
+                 max_msg_bytes: int = 256, depth: int = 3, eager: bool = False, sender_comb: bool = False,
+                 sender_cache: int = 0):
         """eager: also seal whenever no batch is in flight (latency mode); sender_comb: per-sender combs in the queue's
-        context (1024 keys; at2v_comb.h)"""
+        context (at2v_comb.h) for `sender_cache` keys (0 = 1024; 2.1 MB of HBM per key)"""
         from . import _POLICIES
         self._lib = _lib()
         o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth,
-                       (QUEUE_EAGER if eager else 0) | (QUEUE_SENDER_COMB if sender_comb else 0))
+                       (QUEUE_EAGER if eager else 0) | (QUEUE_SENDER_COMB if sender_comb else 0), sender_cache)
         h = ctypes.c_void_p()
         _chk(self._lib.at2v_queue_create(ctypes.byref(o), ctypes.byref(h)), "at2v_queue_create")
         self._h = h

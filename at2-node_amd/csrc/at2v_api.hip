@@ -70,16 +70,28 @@ struct DevBuf {
   }
 };
 
-// Per-sender A cache of one device (at2v_opts.sender_cache; at2v_cache.h). Launches are serialised by scratch_free, so
-// one set of buffers serves every launch of the context. When a launch finds the cache full, the host learns it from
-// the counters' asynchronous copy and clears the tags before a later launch (eviction = start over).
+// Per-sender A cache of one device (at2v_opts.sender_cache; at2v_cache.h). Cached launch L claims new keys
+// into claim slot b = L % kClaimSlots; right after the launch the build stream builds the slot's payloads, flips them
+// valid and frees the slot (slot_free[b]), so no launch waits for a build unless kClaimSlots launches in a row are
+// still waiting for theirs. (The claim slots were round 4's first design's claim sets plus build slots and a copy kernel
+// between them; a copy queued on the build stream behind a 0.8 ms comb build stalled the latency path just the same.)
+// When a launch finds the free list empty, the host learns it from the counters' asynchronous copy and compacts the
+// cache before a later launch, once no cached launch or build is in flight.
+constexpr int kClaimSlots = 8;
 struct SenderCache {
   at2v::CacheArgs args{};
-  hipEvent_t free = nullptr;  // recorded after every cached launch: cached launches never overlap (shared tags/slots)
-  DevBuf tags, entries, slot_of, new_list, ctl, comb, bcomb;
+  DevBuf tags[2], entries[2];  // the live tag table / entries ([cur]) and the compaction target ([cur ^ 1])
+  int cur = 0;
+  DevBuf payload, free_slots, used, ctl, bcomb, claim_list[kClaimSlots];
+  hipStream_t build = nullptr;
+  hipEvent_t claims_ready[kClaimSlots] = {};  // launch stream, after the launch that filled slot b
+  hipEvent_t slot_free[kClaimSlots] = {};     // build stream, after slot b's flip
+  hipEvent_t built = nullptr;                 // build stream, after the last flip
   unsigned long long* host_ctl = nullptr;  // pinned copy of the device counters, refreshed after every cached launch
   hipEvent_t ctl_copied = nullptr;
   bool copy_pending = false;
+  bool compact_pending = false;
+  uint64_t launches = 0;  // launch epochs (entries record the last launch that used them)
 };
 
 // scratch sets per device (AT2V_SCRATCH_SETS overrides, 1..4; 1 = every launch waits for the previous one)
@@ -113,6 +125,7 @@ struct at2v_ctx {
   int rank = 0, world = 1;
   DevBuf window;              // at2v_verify_batch_sharded: world x kGatherWindow words, one all-gather round
   DevBuf zeros;               // >= kGatherWindow zero words: what a rank that failed locally sends
+  DevBuf zeros_big;           // zero words for at2v_verify_shard_gather_device calls with words_per_rank > kGatherWindow
   DevBuf status;              // one int32: the cross-rank failure flag (at2v_verify_batch_sharded)
   hipEvent_t gather_done = nullptr;  // recorded after every all-gather, on its stream (at2v_destroy waits for it)
   uint64_t gathers = 0;       // all-gathers issued (at2v_info.gathers)
@@ -161,78 +174,103 @@ bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) &
 
 void free_cache(SenderCache*& c) {
   if (!c) return;
-  c->tags.release();
-  c->entries.release();
-  c->slot_of.release();
-  c->new_list.release();
-  c->comb.release();
-  c->bcomb.release();
-  c->ctl.release();
+  if (c->build) (void)hipStreamSynchronize(c->build);
+  for (DevBuf* b : {&c->tags[0], &c->tags[1], &c->entries[0], &c->entries[1], &c->payload, &c->free_slots, &c->used,
+                    &c->ctl, &c->bcomb})
+    b->release();
+  for (DevBuf& b : c->claim_list) b.release();
+  if (c->built) (void)hipEventDestroy(c->built);
   if (c->host_ctl) (void)hipHostFree(c->host_ctl);
   if (c->ctl_copied) (void)hipEventDestroy(c->ctl_copied);
-  if (c->free) (void)hipEventDestroy(c->free);
+  for (int j = 0; j < kClaimSlots; ++j) {
+    if (c->claims_ready[j]) (void)hipEventDestroy(c->claims_ready[j]);
+    if (c->slot_free[j]) (void)hipEventDestroy(c->slot_free[j]);
+  }
+  if (c->build) (void)hipStreamDestroy(c->build);
   delete c;
   c = nullptr;
 }
 
 // Per-sender cache for `capacity` distinct keys on the current device: 2x as many tag slots (open addressing at
-// load <= 1/2), one entry per slot. AT2V_TEST_CACHE_FP_BITS (tests only) keeps that many fingerprint bits, so distinct
-// keys collide and the byte comparison in the verify kernel is exercised.
+// load <= 1/2), one payload per key. AT2V_TEST_CACHE_FP_BITS (tests only) keeps that many fingerprint bits, so distinct
+// keys collide and the byte comparison in the verify kernels is exercised.
 int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
   SenderCache* c = new (std::nothrow) SenderCache;
   if (!c) return AT2V_E_OOM;
   s.cache = c;
+  if (capacity > (1u << 24)) capacity = 1u << 24;
   uint32_t cap = 1024;
-  while (cap < 2ull * capacity && cap < (1u << 30)) cap <<= 1;
-  c->args.cap = cap;
-  c->args.capacity = capacity < cap / 2 ? capacity : cap / 2;
-  c->args.seed = seed;
-  c->args.fp_mask = ~0ull;
+  while (cap < 2ull * capacity) cap <<= 1;
+  at2v::CacheArgs& a = c->args;
+  a.cap = cap;
+  a.capacity = capacity;
+  a.seed = seed;
+  a.fp_mask = ~0ull;
+  a.comb = comb ? 1 : 0;
   if (const char* b = std::getenv("AT2V_TEST_CACHE_FP_BITS")) {
     const int bits = std::atoi(b);
-    if (bits > 0 && bits < 64) c->args.fp_mask = (1ull << bits) - 1ull;
+    if (bits > 0 && bits < 64) a.fp_mask = (1ull << bits) - 1ull;
   }
   const size_t ctl_bytes = (size_t)at2v::cache_ctl_words() * 8;
-  AT2V_TRY(c->tags.ensure((size_t)cap * 8));
-  AT2V_TRY(c->entries.ensure((size_t)cap * at2v::cache_entry_bytes()));
+  for (int t = 0; t < 2; ++t) {
+    AT2V_TRY(c->tags[t].ensure((size_t)cap * 8));
+    AT2V_TRY(c->entries[t].ensure((size_t)cap * at2v::cache_entry_bytes()));
+    AT2V_TRY(hipMemset(c->tags[t].p, 0, c->tags[t].cap));
+    AT2V_TRY(hipMemset(c->entries[t].p, 0, c->entries[t].cap));  // every entry invalid
+  }
+  AT2V_TRY(c->payload.ensure((size_t)capacity * at2v::cache_payload_bytes(a.comb)));
+  AT2V_TRY(c->free_slots.ensure((size_t)capacity * 4));
+  AT2V_TRY(c->used.ensure((size_t)capacity * 4));
   AT2V_TRY(c->ctl.ensure(ctl_bytes));
-  AT2V_TRY(hipMemset(c->tags.p, 0, c->tags.cap));
-  AT2V_TRY(hipMemset(c->entries.p, 0, c->entries.cap));  // every entry invalid until a build kernel writes it
   AT2V_TRY(hipMemset(c->ctl.p, 0, c->ctl.cap));
-  if (comb) {  // one comb per key up to the capacity (claim index u -> comb u), and the comb of B
-    AT2V_TRY(c->comb.ensure((size_t)c->args.capacity * at2v::comb_bytes()));
+  for (int j = 0; j < kClaimSlots; ++j) AT2V_TRY(c->claim_list[j].ensure((size_t)capacity * 16));
+  a.tags = (unsigned long long*)c->tags[0].p;
+  a.entries = (int4*)c->entries[0].p;
+  a.payload = (int4*)c->payload.p;
+  a.free_slots = (uint32_t*)c->free_slots.p;
+  a.ctl = (unsigned long long*)c->ctl.p;
+  a.new_list = (uint4*)c->claim_list[0].p;
+  if (comb) {  // the comb of B, built once
     AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes()));
     AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, s.stream));
-    AT2V_TRY(hipStreamSynchronize(s.stream));
-    c->args.comb = (int4*)c->comb.p;
-    c->args.bcomb = (const int4*)c->bcomb.p;
+    a.bcomb = (const int4*)c->bcomb.p;
   }
+  AT2V_TRY(at2v::launch_cache_init(a, s.stream));
+  AT2V_TRY(hipStreamSynchronize(s.stream));
   AT2V_TRY(hipHostMalloc((void**)&c->host_ctl, c->ctl.cap, hipHostMallocDefault));
   std::memset(c->host_ctl, 0, c->ctl.cap);
+  AT2V_TRY(hipStreamCreateWithFlags(&c->build, hipStreamNonBlocking));
   AT2V_TRY(hipEventCreateWithFlags(&c->ctl_copied, hipEventDisableTiming));
-  AT2V_TRY(hipEventCreateWithFlags(&c->free, hipEventDisableTiming));
-  AT2V_TRY(hipEventRecord(c->free, s.stream));
-  c->args.tags = (unsigned long long*)c->tags.p;
-  c->args.entries = (int4*)c->entries.p;
-  c->args.ctl = (unsigned long long*)c->ctl.p;
+  for (int j = 0; j < kClaimSlots; ++j) {  // recorded once, so the first waits are no-ops
+    AT2V_TRY(hipEventCreateWithFlags(&c->claims_ready[j], hipEventDisableTiming));
+    AT2V_TRY(hipEventCreateWithFlags(&c->slot_free[j], hipEventDisableTiming));
+    AT2V_TRY(hipEventRecord(c->claims_ready[j], s.stream));
+    AT2V_TRY(hipEventRecord(c->slot_free[j], c->build));
+  }
+  AT2V_TRY(hipEventCreateWithFlags(&c->built, hipEventDisableTiming));
+  AT2V_TRY(hipEventRecord(c->built, c->build));
   return AT2V_OK;
 }
 
-// Before a cached launch: size the per-record slot array, and if an earlier launch found the cache full (its counters'
-// copy has landed), start over: clear the tags and the counters on the stream.
-hipError_t cache_before_launch(SenderCache& c, uint32_t n, hipStream_t stream) {
-  hipError_t e = c.slot_of.ensure((size_t)n * 4);
-  if (e == hipSuccess) e = c.new_list.ensure((size_t)n * 16);
-  if (e != hipSuccess) return e;
-  c.args.slot_of = (int*)c.slot_of.p;
-  c.args.new_list = (uint4*)c.new_list.p;
-  if (c.copy_pending && hipEventQuery(c.ctl_copied) == hipSuccess) {
+// Before a cached launch on `stream`: wait until the launch's claim slot is free; if an earlier launch found the cache
+// full (its counters' copy has landed), compact it first, once every cached launch and build is done.
+hipError_t cache_before_launch(SenderCache& c, hipStream_t stream, int j) {
+  hipError_t e = hipStreamWaitEvent(stream, c.slot_free[j], 0);
+  if (e == hipSuccess && c.copy_pending && hipEventQuery(c.ctl_copied) == hipSuccess) {
     c.copy_pending = false;
-    if (c.host_ctl[at2v::cache_ctl_full()]) {
-      e = hipMemsetAsync(c.tags.p, 0, c.tags.cap, stream);
-      const size_t used = (size_t)at2v::cache_ctl_used(), full = (size_t)at2v::cache_ctl_full();
-      if (e == hipSuccess) e = hipMemsetAsync((unsigned long long*)c.ctl.p + used, 0, 8, stream);
-      if (e == hipSuccess) e = hipMemsetAsync((unsigned long long*)c.ctl.p + full, 0, 8, stream);
+    if (c.host_ctl[at2v::kCtlFull]) c.compact_pending = true;
+  }
+  if (e == hipSuccess && c.compact_pending) {
+    for (int k = 0; k < kClaimSlots && e == hipSuccess; ++k) e = hipStreamWaitEvent(stream, c.claims_ready[k], 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, c.built, 0);
+    const int nx = c.cur ^ 1;
+    at2v::CacheCompactArgs x{(unsigned long long*)c.tags[nx].p, (int4*)c.entries[nx].p, (uint32_t*)c.used.p};
+    if (e == hipSuccess) e = at2v::launch_cache_compact(c.args, x, stream);
+    if (e == hipSuccess) {
+      c.cur = nx;
+      c.args.tags = x.new_tags;
+      c.args.entries = x.new_entries;
+      c.compact_pending = false;
     }
   }
   return e;
@@ -253,16 +291,28 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   // blocks stride over all chunks), so the zeroing is left out there: one dependent memset less on the latency path
   if (c && c->args.comb && n <= ctx->pair_max) zero_verdicts = false;
   if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
-  if (e == hipSuccess && c) e = hipStreamWaitEvent(stream, c->free, 0);
-  if (e == hipSuccess && c) e = cache_before_launch(*c, n, stream);
+  const int cs = c ? (int)(c->launches % kClaimSlots) : 0;
+  if (e == hipSuccess && c) e = cache_before_launch(*c, stream, cs);
+  at2v::CacheArgs ca{};
+  if (c) {
+    c->args.count_word = at2v::kCtlClaims0 + cs;
+    c->args.new_list = (uint4*)c->claim_list[cs].p;
+    c->args.epoch = (uint32_t)++c->launches;
+    ca = c->args;
+  }
   if (e == hipSuccess)
     e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch[j].p,
-                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &c->args : nullptr);
+                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &ca : nullptr);
   if (e == hipSuccess && c) {
-    e = hipMemcpyAsync(c->host_ctl, c->ctl.p, c->ctl.cap, hipMemcpyDeviceToHost, stream);
+    // claims of this launch -> payloads on the build stream (later launches use them; this one did not wait)
+    e = hipEventRecord(c->claims_ready[cs], stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->build, c->claims_ready[cs], 0);
+    if (e == hipSuccess) e = at2v::launch_cache_build(ca, std::min(n, ca.capacity), c->build);
+    if (e == hipSuccess) e = hipEventRecord(c->slot_free[cs], c->build);
+    if (e == hipSuccess) e = hipEventRecord(c->built, c->build);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->host_ctl, c->ctl.p, c->ctl.cap, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipEventRecord(c->ctl_copied, stream);
     c->copy_pending = e == hipSuccess;
-    if (e == hipSuccess) e = hipEventRecord(c->free, stream);
   }
   if (e == hipSuccess) e = hipEventRecord(s.scratch_free[j], stream);
   return e;
@@ -280,17 +330,26 @@ int gather_shard(at2v_ctx* ctx, Shard& s, int local, const uint8_t* d_pk, const 
                  size_t msg_bytes, const uint32_t* d_msg_off, size_t n_local, size_t wpr, uint32_t* d_bitmap,
                  hipStream_t st) {
   uint32_t* mine = d_bitmap + (size_t)ctx->rank * wpr;
-  const void* send = mine;
+  // A zero buffer of this call's size exists before any work (it grows, zeroed, on the first call with a larger
+  // words_per_rank): a rank that fails anywhere below sends it, never its slice, whose contents are then unknown.
+  DevBuf& zb = wpr * 4 <= ctx->zeros.cap ? ctx->zeros : ctx->zeros_big;  // zeros: kGatherWindow words (comm init)
+  bool zeros_ok = zb.cap >= wpr * 4;
+  if (!zeros_ok) {
+    zeros_ok = zb.ensure(wpr * 4) == hipSuccess && hipMemset(zb.p, 0, zb.cap) == hipSuccess;
+    if (!zeros_ok) zb.release();
+    if (!zeros_ok && local == AT2V_OK) local = AT2V_E_OOM;
+  }
   const hipError_t ez = hipMemsetAsync(mine, 0, wpr * 4, st);  // pad words (and an empty rank's whole slice) are 0
   if (ez != hipSuccess && local == AT2V_OK) local = hip_code(ez);
   if (local == AT2V_OK && n_local) {
     const hipError_t e = launch_shard(ctx, s, d_pk, d_sig, d_msg, (uint32_t)msg_bytes, d_msg_off, (uint32_t)n_local,
                                       mine, st, /*zero_verdicts=*/false);
-    if (e != hipSuccess) local = hip_code(e);  // the slice stays as zeroed above (stream order)
+    if (e != hipSuccess) local = hip_code(e);
   }
-  if (ez != hipSuccess && ctx->zeros.ensure(wpr * 4) == hipSuccess &&
-      hipMemset(ctx->zeros.p, 0, ctx->zeros.cap) == hipSuccess)
-    send = ctx->zeros.p;
+  // a failed rank contributes zero words (fail closed). Only if it could neither zero its slice nor hold a zero buffer
+  // (a device that fails every allocation and memset) does it send its slice as it is.
+  const void* send = mine;
+  if (local != AT2V_OK && zeros_ok) send = zb.p;
   // Collectives of one communicator run one at a time in issue order on every rank: a caller that alternates streams
   // (so that consecutive verify launches overlap) must not let two all-gathers run concurrently, or ranks could
   // execute them in different orders. This one waits for the previous one, whatever stream it ran on.
@@ -329,6 +388,9 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
     int rc = init_shard(c->shards[(size_t)g], o.device + g);
     if (rc == AT2V_OK && o.sender_cache)
       rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd(), o.sender_comb != 0);
+    // the cross-rank failure flag of at2v_comm_init_rank / at2v_verify_batch_sharded (first device): allocated here,
+    // so a rank whose communicator set-up fails can still join the outcome all-reduce
+    if (rc == AT2V_OK && g == 0) rc = hip_code(c->status.ensure(4));
     if (rc != AT2V_OK) {
       (void)hipSetDevice(prev);
       at2v_destroy(c);
@@ -360,6 +422,7 @@ void at2v_destroy(at2v_ctx* ctx) {
   if (ctx->gather_done) (void)hipEventDestroy(ctx->gather_done);
   ctx->window.release();
   ctx->zeros.release();
+  ctx->zeros_big.release();
   ctx->status.release();
   for (Shard& s : ctx->shards) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
@@ -469,18 +532,19 @@ int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BY
   int prev = 0;
   (void)hipGetDevice(&prev);
   int rc = hip_code(hipSetDevice(ctx->shards[0].device));
-  // the failure-path buffers exist before the first collective, so a rank that fails later can still join it
+  // the failure-path buffers exist before the first collective, so a rank that fails later can still join it (the
+  // status word itself is allocated by at2v_create, so the outcome all-reduce below can always be joined)
   if (rc == AT2V_OK) rc = hip_code(ctx->zeros.ensure(kGatherWindow * 4));
   if (rc == AT2V_OK) rc = hip_code(hipMemset(ctx->zeros.p, 0, ctx->zeros.cap));
   if (rc == AT2V_OK) rc = hip_code(ctx->window.ensure(kGatherWindow * 4 * (size_t)world));
-  if (rc == AT2V_OK) rc = hip_code(ctx->status.ensure(4));
   if (rc == AT2V_OK && !ctx->gather_done) {
     rc = hip_code(hipEventCreateWithFlags(&ctx->gather_done, hipEventDisableTiming));
     if (rc == AT2V_OK) rc = hip_code(hipEventRecord(ctx->gather_done, ctx->shards[0].stream));  // first wait: no-op
   }
+  if (rc == AT2V_OK && std::getenv("AT2V_TEST_FAIL_COMM_SETUP")) rc = AT2V_E_HIP;  // test hook: a local set-up failure
   // collective: blocks until all `world` ranks have called it (a rank that failed above still joins, then reports)
   const int rn = nccl_code(ncclCommInitRank(&ctx->comm, world, id, rank));
-  if (rn == AT2V_OK && ctx->status.p) {
+  if (rn == AT2V_OK) {  // every rank that holds a communicator joins the outcome all-reduce, whatever failed locally
     // agree on the outcome: if any rank failed its local set-up, every rank drops the communicator, so no rank is left
     // with a peer that will never join its collectives
     int got = 1;
@@ -716,17 +780,25 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
   out->world = ctx->comm ? ctx->world : 0;
   out->gathers = ctx->gathers;
   out->cache_entries = out->cache_chunks = out->cache_chunk_hits = 0;
-  for (const Shard& sh : ctx->shards) {  // sender-cache counters, summed over devices (synchronises the devices)
+  out->cache_capacity = out->cache_claims = out->cache_evicted = out->cache_compactions = 0;
+  for (const Shard& sh : ctx->shards) {
+    // sender-cache counters, summed over devices. Waits for the context's cache work only (its build stream, which
+    // follows every cached launch): builds of earlier launches are done and their keys usable when this returns.
     if (!sh.cache) continue;
     std::vector<unsigned long long> w((size_t)at2v::cache_ctl_words());
     int prev = 0;
     (void)hipGetDevice(&prev);
-    if (hipSetDevice(sh.device) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+    if (hipSetDevice(sh.device) == hipSuccess && hipStreamSynchronize(sh.cache->build) == hipSuccess &&
         hipMemcpy(w.data(), sh.cache->ctl.p, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      // claims since the last restart; those beyond the capacity are not built
-      out->cache_entries += std::min<uint64_t>(w[(size_t)at2v::cache_ctl_used()], sh.cache->args.capacity);
-      out->cache_chunks += w[(size_t)at2v::cache_ctl_chunks()];
-      out->cache_chunk_hits += w[(size_t)at2v::cache_ctl_chunk_hits()];
+      const uint64_t fc = w[at2v::kCtlFreeCount], fh = w[at2v::kCtlFreeHead];
+      const uint64_t cap = sh.cache->args.capacity;
+      out->cache_entries += (cap - std::min(fc, cap)) + std::min(fh, fc);  // keys holding a payload
+      out->cache_chunks += w[at2v::kCtlChunks];
+      out->cache_chunk_hits += w[at2v::kCtlChunkHits];
+      out->cache_claims += w[at2v::kCtlClaimed];
+      out->cache_evicted += w[at2v::kCtlEvicted];
+      out->cache_compactions += w[at2v::kCtlCompactions];
+      out->cache_capacity += cap;
     }
     (void)hipSetDevice(prev);
   }

@@ -1,7 +1,21 @@
 // at2v_cache.h — device buffers of the per-sender A cache (at2v_opts.sender_cache), shared by the launcher
 // (at2v_kernels.hip) and the context (at2v_api.hip). AT2 senders issue consecutive sequences
 // (/root/reference/src/bin/server/accounts/account.rs:36-43), so one key signs many payloads of a node batch; the cache
-// keeps, per distinct A, dalek's decode verdict and the table [j]A the verify kernel would otherwise rebuild per record.
+// keeps, per distinct A, dalek's decode verdict and a payload derived from A alone: the table [j]A the ladder kernel
+// would otherwise rebuild per record, or (sender_comb) the comb of -A that replaces the doublings.
+//
+// Layout (round 4):
+//   tags[cap]      64-bit keyed fingerprints, 0 = free (open addressing, cap >= 2 x capacity: load <= 1/2)
+//   entries[cap]   4 granules: key (A's 32 bytes), meta = {decode verdict, valid, payload index u (-1: none), last epoch}
+//   payload[u]     capacity payloads (a table [j]A or a comb), handed out from the free list free_slots[]
+// The verify kernels look their senders up themselves (chunk prologue) and claim new keys; a claim takes a payload
+// index from the free list and is listed in the launch's claim slot. After the launch the context's build stream builds
+// the payloads (cache_build_kernel / cache_comb_kernel), then cache_flip_kernel sets valid and frees the slot: a key
+// becomes usable by launches that start later, and the launch that first sees it verifies its records without the cache,
+// never waiting for a build.
+// When the free list runs dry the launch flags the cache full; before the next launch the context compacts it: the
+// most recently used entries (by launch epoch, at most 3/4 of the capacity) move to a fresh tag table with their
+// payloads in place, every other payload goes back to the free list.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -10,30 +24,61 @@
 namespace at2v {
 
 struct CacheArgs {
-  unsigned long long* tags;  // cap 64-bit fingerprints, 0 = free (cap a power of two)
+  unsigned long long* tags;  // cap fingerprints (cap a power of two)
   uint32_t cap;
-  uint32_t capacity;         // entries built since the last restart (<= cap / 2); claims beyond it stay unbuilt
-  int4* entries;             // cap entries of cache_entry_granules() x 16 B (zeroed at creation: every entry invalid)
-  int* slot_of;              // per record of the launch: entry index or -1
-  uint4* new_list;           // (entry, record, claim index since the restart, 0) of the entries claimed by this launch
-  int4* comb;                // at2v_opts.sender_comb: capacity combs of kCombBytes (claim index u -> comb u), else null
-  const int4* bcomb;         // ... and the context's comb of B (kBCombPos x kBCombEntries affine Niels entries)
-  unsigned long long* ctl;   // counters, kCtl* in at2v_kernels.hip: used, full, new, found, claimed, failed, chunk hits
+  uint32_t capacity;         // payload slots
+  int4* entries;             // cap x kCacheEntryGranules (zeroed at creation / compaction: every entry invalid)
+  int4* payload;             // capacity x cache_payload_granules()
+  uint32_t* free_slots;      // payload indices; [free_head, free_count) are free (ctl words)
+  uint4* new_list;           // a claim list: (entry slot, payload u, 0, 0) per claim that got a payload
+  int count_word;            // the list's count (ctl word kCtlClaims0 + claim slot)
+  uint32_t epoch;            // launch number (entries record the last one that used them)
+  int comb;                  // 1: payloads are combs of -A (sender_comb), 0: tables [j]A
+  const int4* bcomb;         // sender_comb: the context's comb of B (kBCombPos x kBCombEntries affine Niels entries)
+  unsigned long long* ctl;   // counters, kCtl* in at2v_kernels.hip
   uint64_t seed;             // fingerprint key (random per context)
   uint64_t fp_mask;          // fingerprint bits kept (all in the product; fewer in a test that forces collisions)
 };
 
+// compaction work buffers (one per device; the alternate tag/entry arrays are swapped in by the host)
+struct CacheCompactArgs {
+  unsigned long long* new_tags;
+  int4* new_entries;
+  uint32_t* used;  // capacity flags: payload kept
+};
+
 size_t cache_entry_bytes();
-size_t comb_bytes();   // one key's comb
-size_t bcomb_bytes();  // the comb of B
+size_t cache_payload_bytes(int comb);  // one key's payload: table [j]A or comb
+size_t bcomb_bytes();                  // the comb of B
 hipError_t launch_build_bcomb(int4* out, hipStream_t stream);
 int cache_ctl_words();
 // ctl word indices the host reads (at2v_get_info) and resets
-int cache_ctl_used();
-int cache_ctl_full();
-int cache_ctl_chunk_hits();
-int cache_ctl_chunks();
-// lookup / claim the launch's senders, then build the entries it claimed (stream order: before the verify kernel)
-hipError_t launch_cache_prepare(const CacheArgs& c, const uint8_t* pk, uint32_t n, hipStream_t stream);
+enum CacheCtlWord : int {
+  kCtlFreeHead = 0,  // payload indices handed out since the last compaction
+  kCtlFreeCount,     // free payload indices after the last compaction
+  kCtlFull,          // a claim found the free list empty (or a probe path full): compact before the next launch
+  kCtlClaims0,       // claims (with a payload) listed in claim slots 0..7, reset by the slot's flip kernel
+  kCtlClaims7 = kCtlClaims0 + 7,
+  kCtlFound,         // records whose key had a tag (statistics)
+  kCtlClaimed,       // keys claimed
+  kCtlFailed,        // records that found neither their key nor a free tag on the probe path
+  kCtlChunkHits,     // chunks whose records all had a valid entry
+  kCtlChunks,
+  kCtlEvicted,       // entries dropped by compactions (total)
+  kCtlCompactions,
+  kCtlKept,          // scratch words of a compaction
+  kCtlThreshold,
+  kCtlRemainder,
+  kCtlRemTaken,
+  kCtlHist,          // 64 age buckets
+  kCtlWordsTotal = kCtlHist + 64
+};
+// initialise a fresh cache: free list 0..capacity-1 (stream order)
+hipError_t launch_cache_init(const CacheArgs& c, hipStream_t stream);
+// build stream, after the launch that filled claim slot c (c.new_list, count word c.count_word): build the payloads it
+// claimed, mark them valid, reset the slot's count
+hipError_t launch_cache_build(const CacheArgs& c, uint32_t max_claims, hipStream_t stream);
+// compact a full cache into (x.new_tags, x.new_entries) (stream order; no cached launch or build may be in flight)
+hipError_t launch_cache_compact(const CacheArgs& c, const CacheCompactArgs& x, hipStream_t stream);
 
 }  // namespace at2v

@@ -38,7 +38,7 @@ struct HipBackend {
   int init(const at2v_queue_opts& o) {
     at2v_opts co{o.device, 1, o.policy, 0, 0, 0};
     if (o.flags & AT2V_QUEUE_SENDER_COMB) {
-      co.sender_cache = 1024;
+      co.sender_cache = o.sender_cache ? o.sender_cache : 1024u;
       co.sender_comb = 1;
     }
     const int rc = at2v_create(&co, &ctx);
@@ -154,7 +154,7 @@ extern "C" {
 int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
-  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0};
+  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0, 0};
   if (opts) o = *opts;
   at2v::QueueOpts qo;
   if (o.max_batch) qo.max_batch = o.max_batch;

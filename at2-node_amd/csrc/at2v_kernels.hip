@@ -388,28 +388,137 @@ struct Pace {
 };
 #endif
 
-// ---- per-sender A cache (at2v_opts.sender_cache) ----
-// An entry: key = the 32 bytes of A (2 granules), meta = {dalek decode verdict of A, valid, comb index, 0} (1 granule),
-// then the table [j]A, j = 0..8, in DevTabA's per-lane layout (90 granules; not built when the entry has a comb). Tags:
-// one 64-bit keyed fingerprint per entry (0 = free), open addressing. A fingerprint only nominates an entry: the verify
-// kernel takes it only if it is valid (built) and all 32 key bytes equal the record's A, so a collision or a claim
-// beyond the capacity costs speed, never a verdict. Entries are zeroed at creation (invalid); an entry is written only
-// by the build kernels, which run before the verify kernel of the same launch, and cached launches never overlap.
-constexpr int kCacheEntryGranules = 3 + kTabAGranules;
-enum : int { kCtlUsed = 0, kCtlFull, kCtlNew, kCtlFound, kCtlClaimed, kCtlFailed, kCtlChunkHits, kCtlChunks, kCtlWords };
+// ---- per-sender A cache (at2v_opts.sender_cache; at2v_cache.h) ----
+// An entry (4 granules, one 64-byte line): key = the 32 bytes of A, meta = {dalek decode verdict of A, valid, payload
+// index u (-1: none), epoch of the last launch that used it}. A fingerprint only nominates an entry: a record takes it
+// only if it is valid (its payload built and flipped by an earlier launch's build stream) and all 32 key bytes equal the
+// record's A, so a collision, a claim without a payload or an entry still being built costs speed, never a verdict.
+// Plain loads of an entry may be stale across XCDs inside one launch; every stale state (valid = 0, a zero key) only
+// turns a hit into a miss, because an entry's key never changes while its tag table is live and valid only goes 0 -> 1.
+constexpr int kCacheEntryGranules = 4;
+constexpr int kCtlWords = kCtlWordsTotal;
 
-__device__ AT2V_INLINE bool cache_hit(const int4* __restrict__ cache, int slot, const uint32_t Aw[8], int& ok,
-                                      int& comb_idx) {
+__device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t seed, uint64_t mask) {
+  uint64_t h = seed;
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    h ^= (uint64_t)a[i] | ((uint64_t)a[i + 1] << 32);
+    h *= 0x9e3779b97f4a7c15ull;
+    h ^= h >> 29;
+  }
+  h *= 0xbf58476d1ce4e5b9ull;
+  h ^= h >> 32;
+  return (h & mask) | 1ull;  // never 0 (= free)
+}
+
+// One record per lane, called by every lane of a wave (ballots): find A's entry by fingerprint (open addressing, 32
+// probes) or claim a free tag (64-bit CAS). Lanes of the wave that want the same new key elect one leader (the lowest
+// lane), which claims for all of them. A claim takes a payload index from the free list (one atomic per wave) and writes
+// the entry's key and meta {0, valid 0, u, epoch}; claims that got a payload are appended to the launch's claim set for
+// the build stream. A claim that finds the free list empty (u = -1) or a record whose probe path is full flags the cache
+// full (compaction before the next launch). Returns the entry slot or -1.
+__device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t a[8], int lane) {
+  const uint32_t mask = c.cap - 1;
+  int slot = -1, claimed = 0, found = 0, want = 0;
+  uint64_t fp = cache_fingerprint(a, c.seed, c.fp_mask);
+  uint32_t h = (uint32_t)(fp >> 17) & mask, k = 0;
+  for (; k < 32; ++k) {  // phase 1: find the key, or the first free tag on its probe path
+    const unsigned long long t =
+        __hip_atomic_load(c.tags + ((h + k) & mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == fp) {
+      slot = (int)((h + k) & mask);
+      found = 1;
+      break;
+    }
+    if (t == 0) {
+      want = 1;
+      break;
+    }
+  }
+  int leader = lane;
+  {
+    uint64_t pending = __ballot(want);
+    while (pending) {  // one iteration per distinct wanted key in the wave
+      const int L = __ffsll((long long)pending) - 1;
+      const uint64_t fpL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fp >> 32), L) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fp, L);
+      const int same = want && fp == fpL;
+      if (same) leader = L;
+      pending &= ~__ballot(same);
+    }
+  }
+  const int follower = want && leader != lane;
+  if (want && !follower) {  // phase 2: claim along the probe path (a racing claimant may take the tag first)
+    for (; k < 32; ++k) {
+      const uint32_t j = (h + k) & mask;
+      const unsigned long long old = atomicCAS(c.tags + j, 0ull, (unsigned long long)fp);
+      if (old == 0) {
+        slot = (int)j;
+        claimed = 1;
+        break;
+      }
+      if (old == fp) {
+        slot = (int)j;
+        found = 1;
+        break;
+      }
+    }
+  }
+  {  // followers take their leader's outcome (a shuffle: every lane of the wave takes part)
+    const int ls = __shfl(slot, leader);
+    if (follower) {
+      slot = ls;
+      found = ls >= 0;
+    }
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint64_t cm = __ballot(claimed);
+  unsigned long long pbase = 0;
+  if (lane == 0 && cm) pbase = atomicAdd(c.ctl + kCtlFreeHead, (unsigned long long)__popcll(cm));
+  pbase = __shfl(pbase, 0);
+  int u = -1;
+  if (claimed) {
+    const unsigned long long q = pbase + (unsigned long long)__popcll(cm & below);
+    const unsigned long long fc = __hip_atomic_load(c.ctl + kCtlFreeCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (q < fc) u = (int)c.free_slots[q];
+  }
+  const uint64_t pm = __ballot(claimed && u >= 0);
+  const uint64_t fm = __ballot(found), xm = __ballot(slot < 0);
+  unsigned long long nbase = 0;
+  if (lane == 0) {
+    if (pm) nbase = atomicAdd(c.ctl + c.count_word, (unsigned long long)__popcll(pm));
+    if (cm) atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
+    if (fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
+    if (xm) atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
+    if (cm != pm || xm) atomicExch(c.ctl + kCtlFull, 1ull);
+  }
+  nbase = __shfl(nbase, 0);
+  if (claimed) {
+    int4* e = c.entries + (size_t)slot * kCacheEntryGranules;
+    e[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
+    e[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
+    e[2] = make_int4(0, 0, u, (int)c.epoch);  // valid once cache_flip_kernel has run (after the payload's build)
+    if (u >= 0) c.new_list[nbase + (unsigned long long)__popcll(pm & below)] = make_uint4((uint32_t)slot, (uint32_t)u, 0u, 0u);
+  }
+  return slot;
+}
+
+// The record's entry is usable: valid and the key bytes equal. ok = A's decode verdict, u = payload index. A hit records
+// this launch's epoch in the entry (the compaction keeps the most recently used entries).
+__device__ AT2V_INLINE bool cache_hit(const CacheArgs& c, int slot, const uint32_t Aw[8], int& ok, int& u) {
   ok = 0;
-  comb_idx = 0;
+  u = 0;
   if (slot < 0) return false;
-  const int4* e = cache + (size_t)slot * kCacheEntryGranules;
+  int4* e = c.entries + (size_t)slot * kCacheEntryGranules;
   const int4 k0 = e[0], k1 = e[1], m = e[2];
   ok = m.x;
-  comb_idx = m.z;
-  return m.y == 1 && (uint32_t)k0.x == Aw[0] && (uint32_t)k0.y == Aw[1] && (uint32_t)k0.z == Aw[2] &&
-         (uint32_t)k0.w == Aw[3] && (uint32_t)k1.x == Aw[4] && (uint32_t)k1.y == Aw[5] && (uint32_t)k1.z == Aw[6] &&
-         (uint32_t)k1.w == Aw[7];
+  u = m.z;
+  const bool hit = m.y == 1 && m.z >= 0 && (uint32_t)k0.x == Aw[0] && (uint32_t)k0.y == Aw[1] &&
+                   (uint32_t)k0.z == Aw[2] && (uint32_t)k0.w == Aw[3] && (uint32_t)k1.x == Aw[4] &&
+                   (uint32_t)k1.y == Aw[5] && (uint32_t)k1.z == Aw[6] && (uint32_t)k1.w == Aw[7];
+  if (hit && (uint32_t)m.w != c.epoch) reinterpret_cast<int*>(e + 2)[3] = (int)c.epoch;
+  if (!hit) u = 0;
+  return hit;
 }
 
 // Half-size verification: one chunk of 64 records per wave, no final inversion. kCache: the per-sender A
@@ -424,9 +533,7 @@ __device__ AT2V_INLINE void verify_chunks(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
     uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
-    uint32_t* __restrict__ chunk_queue, const int* __restrict__ slot_of, const int4* __restrict__ cache,
-    unsigned long long* __restrict__ cache_ctl, const int4* __restrict__ comb = nullptr,
-    const int4* __restrict__ bcomb = nullptr) {
+    uint32_t* __restrict__ chunk_queue, const CacheArgs* cp) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
@@ -520,24 +627,27 @@ __device__ AT2V_INLINE void verify_chunks(
 #if AT2V_FIELD_FU
     int good;
     if (kCache) {
-      int a_ok = 0, comb_idx = 0;
-      const bool hit = cache_hit(cache, slot_of[ii], Aw, a_ok, comb_idx);
+      const CacheArgs& cc = *cp;
+      // the chunk's senders: looked up (new keys claimed for the build stream) in the chunk prologue
+      const int slot = cache_lookup_wave(cc, Aw, lane);
+      int a_ok = 0, u = 0;
+      const bool hit = cache_hit(cc, slot, Aw, a_ok, u);
       const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
       if (lane == 0) {
-        atomicAdd(cache_ctl + kCtlChunks, 1ull);
-        if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 1ull);
+        atomicAdd(cc.ctl + kCtlChunks, 1ull);
+        if (all_hit) atomicAdd(cc.ctl + kCtlChunkHits, 1ull);
       }
       if (kComb) {
         if (all_hit) {
-          const DevComb tc{comb + (size_t)comb_idx * (kCombBytes / 16), {astage + wib * 640, rstage + wib * 640}, lane};
-          const DevBComb tbc{bcomb, {astage + wib * 640, rstage + wib * 640}, lane};
+          const DevComb tc{cc.payload + (size_t)u * (kCombBytes / 16), {astage + wib * 640, rstage + wib * 640}, lane};
+          const DevBComb tbc{cc.bcomb, {astage + wib * 640, rstage + wib * 640}, lane};
           good = verify_comb_fu(Rw, Aw, Sw, len, msgword, policy, a_ok, tc, tbc) & (i < n);
         } else {
           good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
         }
       } else {
         DevTabA tc{ta};
-        if (all_hit) tc.base = const_cast<int4*>(cache) + (size_t)slot_of[ii] * kCacheEntryGranules + 3;
+        if (all_hit) tc.base = cc.payload + (size_t)u * kTabAGranules;
         good = verify_half_fu<true>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace, all_hit, a_ok) &
                (i < n);
       }
@@ -587,58 +697,79 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   verify_chunks<false>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
-                       nullptr, nullptr, nullptr);
+                       nullptr);
 }
 
-// the same with the per-sender A cache (at2v_opts.sender_cache)
+// the same with the per-sender A cache (at2v_opts.sender_cache, tables [j]A)
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_cached(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
-    const int* __restrict__ slot_of, const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, CacheArgs c) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
-  verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
-                      slot_of, cache, cache_ctl);
+  verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, &c);
 }
 
+// LDS words of the four-wave split check (in the kernel's `part` array, word-major: [word][lane])
+constexpr int kSplitDig = 0;          // c0 digits (8 words), |c1| digits (8 words)
+constexpr int kSplitFlags = 16 * 64;  // bit 0: the lattice / window check, bit 1: c1 < 0
+constexpr int kSplitP1 = 40 * 64;     // [c1]R, cached form (40 words)
+constexpr int kSplitPb = 80 * 64;     // -[t]B, cached form (40 words)
+
 // Low-latency verify from combs (at2v_opts.sender_comb, launches of <= small_batch_max records): a block of 4 waves (one
-// per SIMD) owns a chunk of 64 records and splits each record's work by wave (at2v_comb.h, comb_check_split):
+// per SIMD) owns a chunk of 64 records. Wave 0 looks the chunk's senders up (claiming new keys for the build stream) and
+// hands each record's entry (payload index or -1, decode verdict) to the other waves through LDS, so all four waves take
+// the same branch. A chunk whose records all hit splits each record's work by wave (at2v_comb.h, comb_check_split):
 //   wave 0: decode R and check its canonicity (one exponentiation), then, after the barrier, R' = Pa0 + Pa1 + Pb and
 //           the projective comparison -> verdict words
 //   wave 1: s < l, the 16 B-comb additions -> Pb
 //   wave 2: SHA-512 -> k, A-comb positions 0..15 -> Pa0;   wave 3: SHA-512 -> k, positions 16..31 -> Pa1
 // so a record's latency is the longest part (SHA-512 + 16 additions) instead of SHA-512 + 48 additions + an inversion.
-// A chunk whose records do not all hit the cache (claims beyond the capacity, probe failures) runs the uncached half-size
-// path on wave 0. Verdict words are written by wave 0's lane 0 for every chunk.
+// Any other chunk (a sender seen for the first time: its comb is built on the build stream after this launch and serves
+// later launches; a claim without a payload; a probe failure) runs the half-size check V = [c0]A + [c1]R - [t]B = 0
+//  split over the four waves: wave 0 decodes A and builds [j]A, wave 1 decodes R and builds [j]R while
+// wave 2 hashes (SHA-512 -> k), reduces the lattice (c0, c1, t) and hands the digits over LDS; then wave 0 runs the
+// [c0]A ladder, wave 1 the [c1]R ladder (four doublings and one addition per window), wave 2 adds [t]B from the comb of
+// B, and wave 0 checks the sum. The chain of a record is then decode + table + one 128-bit ladder, instead of SHA-512,
+// the lattice and the fixed-base additions on top (the two-lane split of the pair kernel). A first-seen
+// sender costs this instead of waiting for its comb (round 3: 0.82-0.94 ms of device time, profiles/r03zg).
+// Verdict words are written by wave 0's lane 0 for every chunk.
 constexpr int kLatBlock = 256;
 __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, const int* __restrict__ slot_of,
-    const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl, const int4* __restrict__ comb,
-    const int4* __restrict__ bcomb) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, CacheArgs c) {
   __shared__ int4 stage[4 * 2 * 640];        // per wave two 10 KiB LDS-DMA stages
-  __shared__ uint32_t part[3 * 40 * 64];      // Pb, Pa0, Pa1 (p3, 40 words) per lane, word-major
-  __shared__ uint32_t sok[64];                // wave 1's s < l
+  __shared__ uint32_t part[3 * 40 * 64];      // Pb, Pa0, Pa1 (p3, 40 words) per lane, word-major; or the R side's P1
+  __shared__ uint32_t sok[64];                // wave 1's s < l, or the R side's checks
+  __shared__ int sent[2 * 64];                // wave 0's cache outcome per record: payload index (-1: miss), A verdict
+  __shared__ int snw;                         // split check: the chunk's window count (wave 2)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int4* st0 = stage + (size_t)w * 2 * 640;
   int4* st1 = st0 + 640;
   const uint32_t nchunks = (n + 63) / 64, nwords = (n + 31) / 32;
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const uint32_t i = c * 64 + lane;
+  auto wmax = [](int v) { return wave_max_i32(v); };
+  for (uint32_t c0 = blockIdx.x; c0 < nchunks; c0 += gridDim.x) {
+    const uint32_t i = c0 * 64 + lane;
     const uint32_t ii = i < n ? i : n - 1;
     uint32_t Rw[8], Sw[8], Aw[8];
     load8(Rw, sig + (size_t)ii * 64);
     load8(Sw, sig + (size_t)ii * 64 + 32);
     load8(Aw, pk + (size_t)ii * 32);
-    int a_ok = 0, comb_idx = 0;
-    const bool hit = cache_hit(cache, slot_of[ii], Aw, a_ok, comb_idx);
-    const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);  // the same records in every wave
+    if (w == 0) {
+      const int slot = cache_lookup_wave(c, Aw, lane);
+      int a_ok0 = 0, u0 = 0;
+      const bool hit0 = cache_hit(c, slot, Aw, a_ok0, u0);
+      sent[lane] = hit0 ? u0 : -1;
+      sent[64 + lane] = a_ok0;
+    }
+    __syncthreads();
+    const int u = sent[lane], a_ok = sent[64 + lane];
+    const int all_hit = __builtin_amdgcn_readfirstlane(__all(u >= 0) ? 1 : 0);  // the same in every wave (LDS)
     if (w == 0 && lane == 0) {
-      atomicAdd(cache_ctl + kCtlChunks, 1ull);
-      if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 1ull);
+      atomicAdd(c.ctl + kCtlChunks, 1ull);
+      if (all_hit) atomicAdd(c.ctl + kCtlChunkHits, 1ull);
     }
     const uint32_t o0 = off[ii];
     const uint32_t len = off[ii + 1] - o0;
@@ -658,10 +789,12 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
     auto touched = [] {};
     MsgSplit<decltype(msg_unguarded), decltype(msg_guarded), decltype(touched)> msgword{msg_fast, msg_unguarded,
                                                                                         msg_guarded, touched};
-    int good = 0;
+    gu_p3 R;   // all-hit: wave 0's decoded R;  fallback: wave 0's decoded A, then [c0]A
+    int ok0 = 0;
+    uint32_t td[8];  // fallback, wave 2: t's signed radix-2^16 digits
+    int4* slot = scratch + (((size_t)blockIdx.x * kWavesPerBlock + w) * 64 + lane) * kLaneGranules;
+    const DevTabA tp{slot, st0, lane, btab + (size_t)kNumBtabs * kBtabEntries * 8};
     if (all_hit) {
-      gu_p3 R;
-      int ok0 = 0;
       if (w == 0) {
         ok0 = comb_decode_r(R, Rw) & comb_prechecks(Rw, Aw, Sw, policy, a_ok);
       } else {
@@ -671,12 +804,12 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
           sok[lane] = (uint32_t)sc_is_canonical(Sw);
           uint32_t sd[8];
           sc_recode16(sd, Sw);
-          const DevBComb tb{bcomb, {st0, st1}, lane};
+          const DevBComb tb{c.bcomb, {st0, st1}, lane};
           comb_sum<false>(P, sd, 0, kBCombPos, tb);
         } else {
           uint32_t kd[kCombDigitWords];
           comb_k_digits(kd, Rw, Aw, len, msgword);
-          const DevComb tc{comb + (size_t)comb_idx * (kCombBytes / 16), {st0, st1}, lane};
+          const DevComb tc{c.payload + (size_t)u * (kCombBytes / 16), {st0, st1}, lane};
           comb_sum<true>(P, kd, w == 2 ? 0 : kCombPos / 2, w == 2 ? kCombPos / 2 : kCombPos, tc);
         }
         const uint32_t* pw = reinterpret_cast<const uint32_t*>(&P);
@@ -684,8 +817,53 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
 #pragma unroll
         for (int q = 0; q < 40; ++q) dst[q * 64 + lane] = pw[q];
       }
-      __syncthreads();
-      if (w == 0) {
+    } else if (w == 0) {  // split check, phase 1: V1, the policy pre-checks, A decoded (dalek rules) and [j]A
+      ok0 = split_a_side(R, Rw, Aw, Sw, policy, tp);
+    } else if (w == 1) {  // R canonical and decoded, [j]R (c1's sign is applied per digit in phase 2)
+      sok[lane] = (uint32_t)split_r_side(Rw, tp);
+    } else if (w == 2) {  // k = SHA-512(R || A || M) mod l, the lattice (c0, c1), t = c1 s mod l: digits to LDS
+      uint32_t c0d[8], c1d[8];
+      int c1_neg, nw_lane;
+      const int okl = split_scalars(c0d, c1d, td, c1_neg, nw_lane, Rw, Aw, Sw, len, msgword);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        part[kSplitDig + q * 64 + lane] = c0d[q];
+        part[kSplitDig + (8 + q) * 64 + lane] = c1d[q];
+      }
+      part[kSplitFlags + lane] = (uint32_t)okl | ((uint32_t)c1_neg << 1);
+      const int nw = wmax(nw_lane);
+      if (lane == 0) snw = nw < 1 ? 1 : nw;
+    }
+    __syncthreads();
+    if (!all_hit) {  // split check, phase 2: the two ladders and [t]B
+      if (w < 2) {
+        uint32_t cd[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cd[q] = part[kSplitDig + (8 * w + q) * 64 + lane];
+        const int flip = w == 1 ? (int)(part[kSplitFlags + lane] >> 1) & 1 : 0;
+        gu_p3 P;
+        split_side_ladder(P, cd, snw, flip, tp);
+        if (w == 0) {
+          R = P;
+        } else {
+          gu_cached cm;
+          gu_p3_to_cached(cm, P);
+          const uint32_t* cw = reinterpret_cast<const uint32_t*>(&cm);
+#pragma unroll
+          for (int q = 0; q < 40; ++q) part[kSplitP1 + q * 64 + lane] = cw[q];
+        }
+      } else if (w == 2) {
+        gu_cached cm;
+        split_neg_tb(cm, td, DevBComb{c.bcomb, {st0, st1}, lane});  // -[t]B
+        const uint32_t* cw = reinterpret_cast<const uint32_t*>(&cm);
+#pragma unroll
+        for (int q = 0; q < 40; ++q) part[kSplitPb + q * 64 + lane] = cw[q];
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      int good;
+      if (all_hit) {
         gu_p3 Pb, Pa0, Pa1;
         uint32_t* pb = reinterpret_cast<uint32_t*>(&Pb);
         uint32_t* p0 = reinterpret_cast<uint32_t*>(&Pa0);
@@ -697,25 +875,24 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
           p1[q] = part[80 * 64 + q * 64 + lane];
         }
         good = ok0 & (int)sok[lane] & comb_check_split(R, Pa0, Pa1, Pb) & (i < n);
+      } else {  // V = [c0]A + [c1]R - [t]B == identity
+        gu_cached c1r, cnb;
+        uint32_t* w1 = reinterpret_cast<uint32_t*>(&c1r);
+        uint32_t* w2 = reinterpret_cast<uint32_t*>(&cnb);
+#pragma unroll
+        for (int q = 0; q < 40; ++q) {
+          w1[q] = part[kSplitP1 + q * 64 + lane];
+          w2[q] = part[kSplitPb + q * 64 + lane];
+        }
+        good = ok0 & (int)sok[lane] & (int)(part[kSplitFlags + lane] & 1) & split_combine(R, c1r, cnb) & (i < n);
       }
-      __syncthreads();  // the LDS parts are reused by the block's next chunk
-    } else if (w == 0) {
-      int4* slot = scratch + ((size_t)blockIdx.x * kWavesPerBlock * 64 + lane) * kLaneGranules;
-      const int4* ident = btab + (size_t)kNumBtabs * kBtabEntries * 8;
-      DevTabA ta{slot, st0, lane, ident};
-      DevTabA tr{slot + kTabAGranules, st1, lane, ident};
-      const DevTabB tb0{btab, st0, lane};
-      const DevTabB tb1{btab + (size_t)kBtabEntries * 8, st1, lane};
-      auto wmax = [](int v) { return wave_max_i32(v); };
-      good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax) & (i < n);
-    }
-    if (w == 0) {
       const uint64_t mask = __ballot(good);
       if (lane == 0) {
-        verdicts[2 * c] = (uint32_t)mask;
-        if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
+        verdicts[2 * c0] = (uint32_t)mask;
+        if (2 * c0 + 1 < nwords) verdicts[2 * c0 + 1] = (uint32_t)(mask >> 32);
       }
     }
+    __syncthreads();  // the LDS parts are reused by the block's next chunk
   }
 }
 
@@ -772,13 +949,13 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
     uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
-    uint32_t* __restrict__ chunk_queue, const int* __restrict__ slot_of, const int4* __restrict__ cache,
-    unsigned long long* __restrict__ cache_ctl, const int4* __restrict__ comb, const int4* __restrict__ bcomb) {
+    uint32_t* __restrict__ chunk_queue, const CacheArgs& cc) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t nchunks = (n + 127) / 128;
+  const int4* __restrict__ comb = cc.payload;
   const uint32_t nwords = (n + 31) / 32;
   int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
   const int4* ident = btab + (size_t)kNumBtabs * kBtabEntries * 8;
@@ -788,7 +965,7 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
   DevTabA tr{slot + kTabAGranules, sr, lane, ident};
   const DevTabB tb0{btab, sa, lane};
   const DevTabB tb1{btab + (size_t)kBtabEntries * 8, sr, lane};
-  const DevBComb tbc{bcomb, {sa, sr}, lane};
+  const DevBComb tbc{cc.bcomb, {sa, sr}, lane};
   auto wmax = [](int v) { return wave_max_i32(v); };
   constexpr uint32_t kHalf = kWavesPerBlock / 2;
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
@@ -799,17 +976,17 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
     const uint32_t i0 = c * 128 + lane, i1 = i0 + 64;
     int a_ok0, a_ok1, cidx0, cidx1;
     int hit;
-    {
+    {  // both halves' senders looked up (new keys claimed for the build stream) in the chunk prologue
       uint32_t Aw[8];
       load8(Aw, pk + (size_t)(i0 < n ? i0 : n - 1) * 32);
-      hit = cache_hit(cache, slot_of[i0 < n ? i0 : n - 1], Aw, a_ok0, cidx0) ? 1 : 0;
+      hit = cache_hit(cc, cache_lookup_wave(cc, Aw, lane), Aw, a_ok0, cidx0) ? 1 : 0;
       load8(Aw, pk + (size_t)(i1 < n ? i1 : n - 1) * 32);
-      hit &= cache_hit(cache, slot_of[i1 < n ? i1 : n - 1], Aw, a_ok1, cidx1) ? 1 : 0;
+      hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane), Aw, a_ok1, cidx1) ? 1 : 0;
     }
     const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
     if (lane == 0) {
-      atomicAdd(cache_ctl + kCtlChunks, 2ull);
-      if (all_hit) atomicAdd(cache_ctl + kCtlChunkHits, 2ull);
+      atomicAdd(cc.ctl + kCtlChunks, 2ull);
+      if (all_hit) atomicAdd(cc.ctl + kCtlChunkHits, 2ull);
     }
     int good0, good1;
     if (all_hit) {
@@ -867,20 +1044,17 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue,
-    const int* __restrict__ slot_of, const int4* __restrict__ cache, unsigned long long* __restrict__ cache_ctl,
-    const int4* __restrict__ comb, const int4* __restrict__ bcomb) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, CacheArgs c) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
 #ifndef AT2V_COMB_PAIRS
 #define AT2V_COMB_PAIRS 1  // 1: two records per lane, one shared inversion (verify_chunks_comb2); 0: one record per lane
 #endif
 #if AT2V_COMB_PAIRS
-  verify_chunks_comb2(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
-                      slot_of, cache, cache_ctl, comb, bcomb);
+  verify_chunks_comb2(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, c);
 #else
   verify_chunks<true, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
-                            chunk_queue, slot_of, cache, cache_ctl, comb, bcomb);
+                            chunk_queue, &c);
 #endif
 }
 
@@ -1286,148 +1460,44 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const uint8_t* __restric
 }
 
 // ------------------------------------------------------------------ per-sender A cache kernels
+// Build stream (after the launch that claimed the keys; at2v_cache.h): payloads of the claim set, then the flip that
+// makes them valid. Compaction (launch stream, no cached launch or build in flight): the most recently used entries move
+// to a fresh tag table, the other payloads go back to the free list.
 
-__device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t seed, uint64_t mask) {
-  uint64_t h = seed;
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) {
-    h ^= (uint64_t)a[i] | ((uint64_t)a[i + 1] << 32);
-    h *= 0x9e3779b97f4a7c15ull;
-    h ^= h >> 29;
-  }
-  h *= 0xbf58476d1ce4e5b9ull;
-  h ^= h >> 32;
-  return (h & mask) | 1ull;  // never 0 (= free)
+__device__ AT2V_INLINE void entry_key(uint32_t a[8], const int4* ent) {
+  const int4 k0 = ent[0], k1 = ent[1];
+  a[0] = (uint32_t)k0.x; a[1] = (uint32_t)k0.y; a[2] = (uint32_t)k0.z; a[3] = (uint32_t)k0.w;
+  a[4] = (uint32_t)k1.x; a[5] = (uint32_t)k1.y; a[6] = (uint32_t)k1.z; a[7] = (uint32_t)k1.w;
 }
 
-// One lane per record: find A's entry by fingerprint (open addressing, 32 probes) or claim a free one (64-bit CAS).
-// slot_of[i] = entry or -1 (no free slot on the probe path: the record takes the uncached path). Lanes of a wave that
-// want the same new key elect one leader, which claims for all of them. Claims are numbered after the fact (kCtlUsed,
-// since the last restart): a claim numbered below the capacity is built, one beyond it keeps its tag but stays invalid
-// (its records go uncached) and marks the cache full, so the host restarts it before a later launch. (A reservation
-// taken BEFORE claiming, round 3's first form, over-subscribed when many waves wanted the same keys at once: with
-// config-1 traffic every wave wants all 64 senders, 64 waves reserved 4096 > capacity, and the denied lanes re-probed
-// before the winning wave had claimed, so whole chunks missed.) Claimed entries are listed for the build kernels; the
-// statistics counters are aggregated per wave.
-__global__ __launch_bounds__(256) void cache_lookup_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const uint32_t mask = c.cap - 1;
-  int slot = -1, claimed = 0, found = 0, want = 0;
-  uint64_t fp = 0;
-  uint32_t h = 0, k = 0;
-  if (i < n) {
+__device__ AT2V_INLINE unsigned long long claim_count(const CacheArgs& c) {
+  return __hip_atomic_load(c.ctl + c.count_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Tables (combs off): one lane per claim of the set: dalek's decode verdict and [j]A (build_a_table, the verify
+// kernel's own steps) into payload u; the key comes from the entry the claim wrote.
+__global__ __launch_bounds__(256) void cache_build_kernel(CacheArgs c) {
+  const unsigned long long cnt = claim_count(c);
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < cnt; t += gridDim.x * 256) {
+    const uint4 e = c.new_list[t];
+    int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
     uint32_t a[8];
-    load8(a, pk + (size_t)i * 32);
-    fp = cache_fingerprint(a, c.seed, c.fp_mask);
-    h = (uint32_t)(fp >> 17) & mask;
-    for (; k < 32; ++k) {  // phase 1: find the key, or the first free slot on its probe path
-      const unsigned long long t = __hip_atomic_load(c.tags + ((h + k) & mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == fp) {
-        slot = (int)((h + k) & mask);
-        found = 1;
-        break;
-      }
-      if (t == 0) {
-        want = 1;
-        break;
-      }
-    }
+    entry_key(a, ent);
+    DevTabA tw{c.payload + (size_t)e.y * kTabAGranules, nullptr, 0, nullptr};  // store() only
+    const int ok = build_a_table(a, tw);
+    reinterpret_cast<int*>(ent + 2)[0] = ok;
   }
-  // Lanes of this wave that want to claim the same key elect one leader (the lowest lane): AT2 traffic puts many records
-  // of one sender in a wave. One iteration per distinct wanted key in the wave.
-  int leader = lane;
-  {
-    uint64_t pending = __ballot(want);
-    while (pending) {
-      const int L = __ffsll((long long)pending) - 1;
-      const uint64_t fpL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fp >> 32), L) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fp, L);
-      const int same = want && fp == fpL;
-      if (same) leader = L;
-      pending &= ~__ballot(same);
-    }
-  }
-  const int follower = want && leader != lane;
-  if (want && !follower) {  // phase 2: claim along the probe path (a racing claimant may take the slot first)
-    for (; k < 32; ++k) {
-      const uint32_t j = (h + k) & mask;
-      const unsigned long long old = atomicCAS(c.tags + j, 0ull, (unsigned long long)fp);
-      if (old == 0) {
-        slot = (int)j;
-        claimed = 1;
-        break;
-      }
-      if (old == fp) {
-        slot = (int)j;
-        found = 1;
-        break;
-      }
-    }
-  }
-  {  // followers take their leader's outcome (a shuffle: every lane of the wave takes part)
-    const int ls = __shfl(slot, leader);
-    if (follower) {
-      slot = ls;
-      found = ls >= 0;
-    }
-  }
-  if (i < n) c.slot_of[i] = slot;
-  const uint64_t cm = __ballot(claimed), fm = __ballot(found), xm = __ballot(i < n && slot < 0);
-  unsigned long long nbase = 0, ubase = 0;
-  if (lane == 0) {
-    if (cm) {
-      ubase = atomicAdd(c.ctl + kCtlUsed, (unsigned long long)__popcll(cm));
-      if (ubase + (unsigned long long)__popcll(cm) > c.capacity) atomicExch(c.ctl + kCtlFull, 1ull);
-      nbase = atomicAdd(c.ctl + kCtlNew, (unsigned long long)__popcll(cm));
-      atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
-    }
-    if (fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
-    if (xm) {
-      atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
-      atomicExch(c.ctl + kCtlFull, 1ull);
-    }
-  }
-  nbase = __shfl(nbase, 0);
-  ubase = __shfl(ubase, 0);
-  const unsigned long long rank = (unsigned long long)__popcll(cm & ((1ull << lane) - 1ull));
-  if (claimed) c.new_list[nbase + rank] = make_uint4((uint32_t)slot, i, (uint32_t)(ubase + rank), 0u);
-}
-
-// One lane per entry claimed by this launch (combs off): key, dalek decode verdict and [j]A (build_a_table, the verify
-// kernel's own steps). A claim beyond the capacity is written invalid. Threads beyond the launch's claim count leave.
-__global__ __launch_bounds__(256) void cache_build_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
-  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-  if ((unsigned long long)t >= __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const uint4 e = c.new_list[t];
-  int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
-  if (e.z >= c.capacity) {
-    ent[2] = make_int4(0, 0, 0, 0);  // invalid: the tag stays (its key keeps finding this slot) until the restart
-    return;
-  }
-  uint32_t a[8];
-  load8(a, pk + (size_t)e.y * 32);
-  DevTabA tw{ent + 3, nullptr, 0, nullptr};  // store() only
-  const int ok = build_a_table(a, tw);
-  ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
-  ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
-  ent[2] = make_int4(ok, 1, (int)e.z, 0);
 }
 
 // One claim of the comb build: thread g of the claim's group (2^kPartsLog2 threads per position) writes its share of the
-// comb of -A at claim index u (comb_build_lane), and g = 0 the entry's key and meta (dalek's decode verdict, valid, u); a
-// claim beyond the capacity is written invalid. The group is block- or wave-uniform.
+// comb of -A into payload u (comb_build_lane), g = 0 the decode verdict. The group is block- or wave-uniform.
 template <int kPartsLog2>
-__device__ AT2V_INLINE void comb_claim(const uint8_t* __restrict__ pk, const CacheArgs& c, uint32_t t, int g) {
+__device__ AT2V_INLINE void comb_claim(const CacheArgs& c, uint32_t t, int g) {
   const uint4 e = c.new_list[t];
   int4* ent = c.entries + (size_t)e.x * kCacheEntryGranules;
-  if (e.z >= c.capacity) {
-    if (g == 0) ent[2] = make_int4(0, 0, 0, 0);
-    return;
-  }
   uint32_t a[8];
-  load8(a, pk + (size_t)e.y * 32);
-  int4* cb = c.comb + (size_t)e.z * (kCombBytes / 16);
+  entry_key(a, ent);
+  int4* cb = c.payload + (size_t)e.y * (kCombBytes / 16);
   const int pos = g >> kPartsLog2;
   const int ok = comb_build_lane<kPartsLog2>(a, pos, g & ((1 << kPartsLog2) - 1), [&](int j, const gu_cached& p) {
     const int32_t* w = reinterpret_cast<const int32_t*>(&p);
@@ -1435,27 +1505,122 @@ __device__ AT2V_INLINE void comb_claim(const uint8_t* __restrict__ pk, const Cac
 #pragma unroll
     for (int q = 0; q < kCombGranules; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   });
-  if (g == 0) {
-    ent[0] = make_int4((int)a[0], (int)a[1], (int)a[2], (int)a[3]);
-    ent[1] = make_int4((int)a[4], (int)a[5], (int)a[6], (int)a[7]);
-    ent[2] = make_int4(ok, 1, (int)e.z, 0);
-  }
+  if (g == 0) reinterpret_cast<int*>(ent + 2)[0] = ok;
 }
 
-// With combs on, the whole build of a launch's claims (persistent grid): up to kCombWideMaxKeys claims, one 256-thread
-// block per claim and 8 threads per position (the latency of a first-seen sender: 0.84-0.96 ms for 1-64 new keys,
-// profiles/r03zf); more claims, one wave per claim and 2 lanes per position (fewer redundant position chains once the
-// waves outnumber the SIMDs). (One kernel instead of cache_build_kernel + this one: one dependent launch less per batch,
-// which the small-batch latency pays.)
-__global__ __launch_bounds__(256) void cache_comb_kernel(const uint8_t* __restrict__ pk, CacheArgs c) {
-  const unsigned long long cnt = __hip_atomic_load(c.ctl + kCtlNew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Combs of a claim set (persistent grid): up to kCombWideMaxKeys claims, one 256-thread block per claim and 8 threads per
+// position (profiles/r03zf); more claims, one wave per claim and 2 lanes per position (fewer redundant position chains
+// once the waves outnumber the SIMDs).
+__global__ __launch_bounds__(256) void cache_comb_kernel(CacheArgs c) {
+  const unsigned long long cnt = claim_count(c);
   if (cnt <= (unsigned long long)kCombWideMaxKeys) {
-    for (uint32_t t = blockIdx.x; t < cnt; t += gridDim.x) comb_claim<kCombWideLog2>(pk, c, t, (int)threadIdx.x);
+    for (uint32_t t = blockIdx.x; t < cnt; t += gridDim.x) comb_claim<kCombWideLog2>(c, t, (int)threadIdx.x);
   } else {
     const uint32_t nw = gridDim.x * 4;
     for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < cnt; t += nw)
-      comb_claim<kCombNarrowLog2>(pk, c, t, (int)(threadIdx.x & 63));
+      comb_claim<kCombNarrowLog2>(c, t, (int)(threadIdx.x & 63));
   }
+}
+
+// After the build kernel (stream order: its payload stores are complete and written back): valid = 1 for every claim of
+// the slot, then the slot's count is reset for the launch that reuses it.
+__global__ __launch_bounds__(1024) void cache_flip_kernel(CacheArgs c) {
+  const unsigned long long cnt = claim_count(c);
+  for (uint32_t t = threadIdx.x; t < cnt; t += 1024) {
+    const uint4 e = c.new_list[t];
+    __hip_atomic_store(reinterpret_cast<int*>(c.entries + (size_t)e.x * kCacheEntryGranules + 2) + 1, 1,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(c.ctl + c.count_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// a fresh cache: every payload index free
+__global__ __launch_bounds__(256) void cache_init_kernel(CacheArgs c) {
+  for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < c.capacity; u += gridDim.x * 256) c.free_slots[u] = u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    c.ctl[kCtlFreeCount] = c.capacity;
+    c.ctl[kCtlFreeHead] = 0;
+  }
+}
+
+__device__ AT2V_INLINE int entry_age(const CacheArgs& c, int4 m) {
+  const uint32_t a = c.epoch - (uint32_t)m.w;
+  return a > 63u ? 63 : (int)a;
+}
+
+// compaction 1: age histogram of the entries that hold a payload (valid: every build has been flipped by now)
+__global__ __launch_bounds__(256) void cache_hist_kernel(CacheArgs c) {
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < c.cap; s += gridDim.x * 256) {
+    if (c.tags[s] == 0) continue;
+    const int4 m = c.entries[(size_t)s * kCacheEntryGranules + 2];
+    if (m.y != 1 || m.z < 0) continue;
+    atomicAdd(c.ctl + kCtlHist + entry_age(c, m), 1ull);
+  }
+}
+
+// compaction 2 (one thread): keep every entry younger than T and `rem` of age T, at most 3/4 of the capacity, so a later
+// launch has a quarter of the payloads for new keys
+__global__ void cache_select_kernel(CacheArgs c) {
+  const unsigned long long target = (unsigned long long)c.capacity * 3 / 4;
+  unsigned long long kept = 0, rem = 0;
+  int T = 64;
+  for (int a = 0; a < 64; ++a) {
+    const unsigned long long h = c.ctl[kCtlHist + a];
+    if (kept + h > target) {
+      T = a;
+      rem = target - kept;
+      break;
+    }
+    kept += h;
+  }
+  c.ctl[kCtlThreshold] = (unsigned long long)T;
+  c.ctl[kCtlRemainder] = rem;
+  c.ctl[kCtlRemTaken] = 0;
+  c.ctl[kCtlKept] = 0;
+  c.ctl[kCtlFreeCount] = 0;
+  c.ctl[kCtlFreeHead] = 0;
+  c.ctl[kCtlFull] = 0;
+  c.ctl[kCtlCompactions] += 1;
+}
+
+// compaction 3: kept entries are re-inserted into the fresh tag table (their payloads stay where they are)
+__global__ __launch_bounds__(256) void cache_compact_kernel(CacheArgs c, CacheCompactArgs x) {
+  const int T = (int)c.ctl[kCtlThreshold];
+  const unsigned long long rem = c.ctl[kCtlRemainder];
+  const uint32_t mask = c.cap - 1;
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < c.cap; s += gridDim.x * 256) {
+    const unsigned long long fp = c.tags[s];
+    if (fp == 0) continue;
+    const int4* e = c.entries + (size_t)s * kCacheEntryGranules;
+    const int4 m = e[2];
+    if (m.y != 1 || m.z < 0) continue;  // a claim that never got a payload: its tag is dropped
+    const int age = entry_age(c, m);
+    const bool keep = age < T || (age == T && atomicAdd(c.ctl + kCtlRemTaken, 1ull) < rem);
+    if (!keep) {
+      atomicAdd(c.ctl + kCtlEvicted, 1ull);
+      continue;
+    }
+    const uint32_t h = (uint32_t)(fp >> 17) & mask;
+    for (uint32_t k = 0; k < c.cap; ++k) {  // fingerprints are unique in a table: the first free tag on the path
+      const uint32_t j = (h + k) & mask;
+      if (atomicCAS(x.new_tags + j, 0ull, fp) == 0ull) {
+        int4* d = x.new_entries + (size_t)j * kCacheEntryGranules;
+        d[0] = e[0];
+        d[1] = e[1];
+        d[2] = m;
+        x.used[m.z] = 1;
+        atomicAdd(c.ctl + kCtlKept, 1ull);
+        break;
+      }
+    }
+  }
+}
+
+// compaction 4: every payload index no kept entry holds is free again
+__global__ __launch_bounds__(256) void cache_freelist_kernel(CacheArgs c, CacheCompactArgs x) {
+  for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < c.capacity; u += gridDim.x * 256)
+    if (!x.used[u]) c.free_slots[atomicAdd(c.ctl + kCtlFreeCount, 1ull)] = u;
 }
 
 // D[pos][j] = [j 2^(16 pos)]B, j = 0..2^15, affine Niels on the unsigned field: one lane per entry, (j 2^(16 pos)) mod l
@@ -1492,7 +1657,7 @@ __global__ __launch_bounds__(kBlock) void build_bcomb_kernel(int4* __restrict__ 
 }
 
 size_t cache_entry_bytes() { return (size_t)kCacheEntryGranules * 16; }
-size_t comb_bytes() { return kCombBytes; }
+size_t cache_payload_bytes(int comb) { return comb ? kCombBytes : (size_t)kTabAGranules * 16; }
 size_t bcomb_bytes() { return (size_t)kBCombPos * kBCombEntries * 8 * 16; }
 
 hipError_t launch_build_bcomb(int4* out, hipStream_t stream) {
@@ -1505,25 +1670,41 @@ hipError_t launch_build_bcomb(int4* out, hipStream_t stream) {
   return hipSuccess;
 }
 int cache_ctl_words() { return kCtlWords; }
-int cache_ctl_used() { return kCtlUsed; }
-int cache_ctl_full() { return kCtlFull; }
-int cache_ctl_chunk_hits() { return kCtlChunkHits; }
-int cache_ctl_chunks() { return kCtlChunks; }
 
-hipError_t launch_cache_prepare(const CacheArgs& c, const uint8_t* pk, uint32_t n, hipStream_t stream) {
-  hipError_t e = hipMemsetAsync(c.ctl + kCtlNew, 0, sizeof(unsigned long long), stream);
-  if (e != hipSuccess) return e;
-  const uint32_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(cache_lookup_kernel, dim3(blocks), dim3(256), 0, stream, pk, n, c);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (!c.comb) {
-    hipLaunchKernelGGL(cache_build_kernel, dim3(blocks), dim3(256), 0, stream, pk, c);
-    return hipGetLastError();
+static uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap_blocks) {
+  const uint64_t b = (items + per_block - 1) / per_block;
+  return (uint32_t)(b < 1 ? 1 : b > cap_blocks ? cap_blocks : b);
+}
+
+hipError_t launch_cache_init(const CacheArgs& c, hipStream_t stream) {
+  hipLaunchKernelGGL(cache_init_kernel, dim3(grid_for(c.capacity, 256, 1024)), dim3(256), 0, stream, c);
+  return hipGetLastError();
+}
+
+hipError_t launch_cache_build(const CacheArgs& c, uint32_t max_claims, hipStream_t stream) {
+  if (max_claims == 0) max_claims = 1;
+  if (c.comb) {  // a block per claim (few claims) or a wave per claim; the grid loops over more
+    hipLaunchKernelGGL(cache_comb_kernel, dim3(max_claims < 512u ? max_claims : 512u), dim3(256), 0, stream, c);
+  } else {
+    hipLaunchKernelGGL(cache_build_kernel, dim3(grid_for(max_claims, 256, 1024)), dim3(256), 0, stream, c);
   }
-  // a block per claim (few claims) or a wave per claim; a launch claims at most n entries (the grid loops over more)
-  const uint32_t blocks_c = n < 512u ? n : 512u;
-  hipLaunchKernelGGL(cache_comb_kernel, dim3(blocks_c), dim3(256), 0, stream, pk, c);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cache_flip_kernel, dim3(1), dim3(1024), 0, stream, c);
+  return hipGetLastError();
+}
+
+hipError_t launch_cache_compact(const CacheArgs& c, const CacheCompactArgs& x, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(x.new_tags, 0, (size_t)c.cap * 8, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(x.new_entries, 0, (size_t)c.cap * kCacheEntryGranules * 16, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(x.used, 0, (size_t)c.capacity * 4, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c.ctl + kCtlHist, 0, 64 * 8, stream);
+  if (e != hipSuccess) return e;
+  const uint32_t gs = grid_for(c.cap, 256, 2048), gu = grid_for(c.capacity, 256, 2048);
+  hipLaunchKernelGGL(cache_hist_kernel, dim3(gs), dim3(256), 0, stream, c);
+  hipLaunchKernelGGL(cache_select_kernel, dim3(1), dim3(1), 0, stream, c);
+  hipLaunchKernelGGL(cache_compact_kernel, dim3(gs), dim3(256), 0, stream, c, x);
+  hipLaunchKernelGGL(cache_freelist_kernel, dim3(gu), dim3(256), 0, stream, c, x);
   return hipGetLastError();
 }
 
@@ -1576,14 +1757,11 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
     if (me != hipSuccess) return me;
   }
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
-  if (cache) {
-    const hipError_t ce = launch_cache_prepare(*cache, pk, n, stream);
-    if (ce != hipSuccess) return ce;
+  if (cache) {  // the kernels look their senders up themselves (at2v_cache.h); builds follow on the build stream
     if (cache->comb && n <= pair_max) {  // small batches: the four-wave split, one block per 64 records
       const uint32_t gl = nchunks < (uint32_t)grid ? nchunks : (uint32_t)grid;
       hipLaunchKernelGGL(verify_comb_lat_kernel, dim3(gl), dim3(kLatBlock), 0, stream, pk, sig, msg, msg_total, off, n,
-                         policy, verdicts, scratch, btab, cache->slot_of, (const int4*)cache->entries, cache->ctl,
-                         (const int4*)cache->comb, cache->bcomb);
+                         policy, verdicts, scratch, btab, *cache);
       return hipGetLastError();
     }
     if (cache->comb) {
@@ -1594,12 +1772,11 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
       const int g2 = g;
 #endif
       hipLaunchKernelGGL(verify_kernel_comb, dim3(g2), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                         verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl,
-                         (const int4*)cache->comb, cache->bcomb);
+                         verdicts, scratch, btab, queue, *cache);
       return hipGetLastError();
     }
     hipLaunchKernelGGL(verify_kernel_cached, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                       verdicts, scratch, btab, queue, cache->slot_of, (const int4*)cache->entries, cache->ctl);
+                       verdicts, scratch, btab, queue, *cache);
     return hipGetLastError();
   }
 #endif

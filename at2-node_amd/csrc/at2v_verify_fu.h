@@ -9,6 +9,7 @@
 //   TabP : store(e, gu_cached) / prefetch(e) / load_prefetched(gu_cached)   (per lane, e in 0..8)
 //   TabB : prefetch(e) / load_prefetched(gu_niels)                          (shared, e in 0..2^15)
 #pragma once
+#include "at2v_comb.h"
 #include "at2v_gu.h"
 #include "at2v_verify.h"
 
@@ -447,6 +448,127 @@ AT2V_HD AT2V_INLINE int verify_pair_combine(const gu_p3& mine, const gu_cached& 
 }  // namespace at2v
 
 namespace at2v {
+
+// [c]P from the table [j]P (tp, j = 0..8) over windows nw-1..0 of c's signed radix-16 digits (sc_recode4_hi8 nibbles,
+// d_i + 7): four doublings and one addition per window; flip = 1 negates every digit (the scalar's sign, applied per
+// entry because the table was built before the sign was known).
+template <class TabP>
+AT2V_HD AT2V_INLINE void split_side_ladder(gu_p3& out, const uint32_t cd[8], int nw, int flip, TabP& tp) {
+  gu_p2 R2;
+  gu_p3 R3;
+  gu_p1p1 tt;
+  gu_cached ca;
+  auto digit4 = [](const uint32_t d[8], int i) -> int { return (int)((sel8(d, i >> 3) >> (4 * (i & 7))) & 15) - 7; };
+  {
+    const int d = digit4(cd, nw - 1);
+    tp.prefetch(d < 0 ? -d : d);
+    gu_p3_identity(R3);
+    tp.load_prefetched(ca);
+    gu_cached_cneg(ca, (d < 0) ^ flip);
+    gu_add(tt, R3, ca);
+    gu_p1p1_to_p2(R2, tt);
+  }
+  for (int i = nw - 2; i >= 0; --i) {
+    const int d = digit4(cd, i);
+    tp.prefetch(d < 0 ? -d : d);  // lands while the window's four doublings run
+    for (int r = 0; r < 3; ++r) {
+      gu_p2_dbl(tt, R2);
+      gu_p1p1_to_p2(R2, tt);
+    }
+    gu_p2_dbl(tt, R2);
+    gu_p1p1_to_p3(R3, tt);
+    tp.load_prefetched(ca);
+    gu_cached_cneg(ca, (d < 0) ^ flip);
+    gu_add(tt, R3, ca);
+    if (i > 0) gu_p1p1_to_p2(R2, tt);
+  }
+  gu_p1p1_to_p3(out, tt);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// The half-size check split over four waves (the low-latency comb kernel's path for chunks whose senders are not all
+// cached): V = [c0]A + [c1]R - [t]B = 0 as in verify_half_fu (§4b), with the parts that do not depend on
+// each other run side by side —
+//   wave 0: split_a_side (V1, policy pre-checks, decode A, [j]A)   then split_side_ladder over c0 with [j]A
+//   wave 1: split_r_side (R canonical, decode R, [j]R)              then split_side_ladder over |c1| with [j]R, sign of c1
+//   wave 2: split_scalars (SHA-512 -> k, lattice, t)               then split_neg_tb: -[t]B from the comb of B
+// and split_combine on wave 0. The verdict is exactly verify_half_fu's: the same checks, the same group element V (any
+// evaluation of the three products gives it), the same identity test.
+
+template <class TabP>
+AT2V_HD AT2V_INLINE int split_a_side(gu_p3& A, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
+                                     int policy, TabP& tp) {
+  int ok = sc_is_canonical(Sw);
+  if (policy == POLICY_LIBSODIUM_1_0_18) {
+    ok &= !enc_small_order(Rw);
+    ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
+  }
+  ok &= gu_frombytes(A, Aw);
+  build_a_table_from(A, tp);
+  return ok;
+}
+
+template <class TabP>
+AT2V_HD AT2V_INLINE int split_r_side(const uint32_t Rw[8], TabP& tp) {
+  gu_p3 R;
+  int ok = enc_y_canonical(Rw);
+  ok &= gu_frombytes(R, Rw);
+  ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
+  build_a_table_from(R, tp);
+  return ok;
+}
+
+// digits of c0 and |c1| (sc_recode4_hi8), t = c1 s mod l (sc_recode16), the sign of c1 and the lane's window count;
+// returns 0 for a lane whose scalars would need a 65th window (fails closed, as verify_half_fu)
+template <class MsgWord>
+AT2V_HD AT2V_INLINE int split_scalars(uint32_t c0d[8], uint32_t c1d[8], uint32_t td[8], int& c1_neg, int& nw_lane,
+                                      const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
+                                      MsgWord msgword) {
+  uint32_t k[8];
+  {
+    uint32_t pre[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      pre[q] = Rw[q];
+      pre[8 + q] = Aw[q];
+    }
+    uint64_t h[8];
+    sha512_msg<16>(h, pre, len, msgword);
+    uint32_t hw[16];
+    sha512_digest_words(hw, h);
+    sc_reduce512(k, hw);
+  }
+  HalfScalars hs;
+  lattice_reduce(hs, k);
+  uint32_t t[8];
+  sc_mul_signed(t, hs, Sw);
+  sc_recode4_hi8(c0d, hs.c0);
+  sc_recode4_hi8(c1d, hs.c1);
+  sc_recode16(td, t);
+  c1_neg = hs.c1_neg;
+  const int ok = hs.bits <= 255;
+  nw_lane = ok ? hs.bits / 4 + 1 : 0;
+  return ok;
+}
+
+// -[t]B in cached form, from the comb of B (TabBC: prefetch(stage, i, j) / load_prefetched(stage, gu_niels&))
+template <class TabBC>
+AT2V_HD AT2V_INLINE void split_neg_tb(gu_cached& out, const uint32_t td[8], const TabBC& tb) {
+  gu_p3 P;
+  gu_p3_identity(P);
+  comb_sum<false>(P, td, 0, kBCombPos, tb);
+  gu_p3_to_cached(out, P);
+  gu_cached_cneg(out, 1);
+}
+
+// V = P0 + P1 + (-[t]B) == identity (P1 and -[t]B in cached form)
+AT2V_HD AT2V_INLINE int split_combine(const gu_p3& P0, const gu_cached& P1, const gu_cached& nTB) {
+  gu_p1p1 t;
+  gu_add(t, P0, P1);
+  gu_p3 S;
+  gu_p1p1_to_p3(S, t);
+  return verify_pair_combine(S, nTB);
+}
 
 // Per-sender cache entry (at2v_opts.sender_cache; AT2 senders repeat, accounts/account.rs:36-43): dalek's decode verdict
 // for A and the table [j]A, j = 0..8, built by exactly the steps verify_half_fu uses for its own [j]A, in the layout it

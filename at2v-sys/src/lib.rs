@@ -31,7 +31,7 @@ pub struct At2vLedger {
 
 /// include/at2v.h AT2V_ABI_VERSION: the layouts of the #[repr(C)] structs below. `BatchVerifier::new` and
 /// `Queue::new` refuse a library that reports another version (the structs are copied whole by the library).
-pub const AT2V_ABI_VERSION: c_int = 4;
+pub const AT2V_ABI_VERSION: c_int = 5;
 
 pub const AT2V_POLICY_DALEK_V1: c_int = 0;
 pub const AT2V_POLICY_LIBSODIUM_1_0_18: c_int = 1;
@@ -100,6 +100,10 @@ pub struct At2vInfo {
     pub cache_entries: u64,
     pub cache_chunks: u64,
     pub cache_chunk_hits: u64,
+    pub cache_capacity: u64,
+    pub cache_claims: u64,
+    pub cache_evicted: u64,
+    pub cache_compactions: u64,
 }
 
 /// `Default`: device 0, DALEK_V1, and the library defaults for every size (65536 records, 1 ms, 256 B, depth 3).
@@ -113,6 +117,8 @@ pub struct At2vQueueOpts {
     pub max_msg_bytes: u32,
     pub depth: u32,
     pub flags: u32,
+    /// with AT2V_QUEUE_SENDER_COMB: keys the queue's context caches (2.1 MB of HBM each); 0 = 1024
+    pub sender_cache: u32,
 }
 
 /// `At2vQueueOpts::flags`: also seal the filling batch whenever no batch is in flight (latency mode).
@@ -260,6 +266,19 @@ pub fn verify_one(public_key: &[u8; 32], signature: &[u8; 64], message: &[u8]) -
     check(unsafe { at2v_verify_one(public_key.as_ptr(), signature.as_ptr(), m, message.len()) }).map(|v| v == 1)
 }
 
+/// The C side copies message bytes up to `msg_off[n]` and takes no length: a safe wrapper must prove every offset is in
+/// `msg` and non-decreasing before it hands the pointers over.
+fn check_records(pk: &[u8], sig: &[u8], msg: &[u8], msg_off: &[u32]) -> Result<usize, Error> {
+    let n = msg_off.len().saturating_sub(1);
+    if pk.len() != 32 * n || sig.len() != 64 * n {
+        return Err(Error(AT2V_E_INVALID));
+    }
+    if msg_off.windows(2).any(|w| w[1] < w[0]) || msg_off.last().map_or(false, |&e| e as usize > msg.len()) {
+        return Err(Error(AT2V_E_INVALID));
+    }
+    Ok(n)
+}
+
 fn check_abi() -> Result<(), Error> {
     if unsafe { at2v_abi_version() } != AT2V_ABI_VERSION {
         return Err(Error(AT2V_E_INVALID));
@@ -296,10 +315,7 @@ impl BatchVerifier {
     /// returns the whole bitmap (requires `init_rank`). Err(AT2V_E_PEER): another rank failed; discard the batch.
     pub fn verify(&mut self, pk: &[u8], sig: &[u8], msg: &[u8], msg_off: &[u32], sharded: bool)
                   -> Result<Vec<bool>, Error> {
-        let n = msg_off.len().saturating_sub(1);
-        if pk.len() != 32 * n || sig.len() != 64 * n {
-            return Err(Error(AT2V_E_INVALID));
-        }
+        let n = check_records(pk, sig, msg, msg_off)?;
         let mut words = vec![0u32; (n + 31) / 32];
         let m = if msg.is_empty() { std::ptr::null() } else { msg.as_ptr() };
         let rc = unsafe {
@@ -364,10 +380,7 @@ impl Queue {
     /// Records in the at2v_verify_batch layout; returns the ticket of the first (the rest follow consecutively).
     /// Blocks only while every batch slot is in flight (backpressure).
     pub fn submit(&self, pk: &[u8], sig: &[u8], msg: &[u8], msg_off: &[u32]) -> Result<u64, Error> {
-        let n = msg_off.len().saturating_sub(1);
-        if pk.len() != 32 * n || sig.len() != 64 * n {
-            return Err(Error(AT2V_E_INVALID));
-        }
+        let n = check_records(pk, sig, msg, msg_off)?;
         let m = if msg.is_empty() { std::ptr::null() } else { msg.as_ptr() };
         let mut first = 0u64;
         check(unsafe { at2v_queue_submit(self.0, pk.as_ptr(), sig.as_ptr(), m, msg_off.as_ptr(), n, &mut first) })?;
@@ -410,4 +423,21 @@ pub fn unique_id() -> Result<[u8; AT2V_UNIQUE_ID_BYTES], Error> {
     let mut id = [0u8; AT2V_UNIQUE_ID_BYTES];
     check(unsafe { at2v_comm_get_unique_id(id.as_mut_ptr()) })?;
     Ok(id)
+}
+
+#[cfg(test)]
+mod tests {
+    use super::*;
+
+    /// an offset array that runs past `msg` (or goes backwards) must be refused by the safe layer before any
+    /// pointer reaches the C side, which reads message bytes up to `msg_off[n]` without a length.
+    #[test]
+    fn safe_layer_rejects_offsets_outside_msg() {
+        let (pk, sig, msg) = ([0u8; 32], [0u8; 64], [0u8; 4]);
+        assert!(check_records(&pk, &sig, &msg, &[0, 4]).is_ok());
+        assert!(check_records(&pk, &sig, &msg, &[0, 5]).is_err()); // past the end of msg
+        assert!(check_records(&pk, &sig, &msg, &[3, 2]).is_err()); // decreasing
+        assert!(check_records(&pk, &sig[..32], &msg, &[0, 4]).is_err()); // short signature
+        assert!(check_records(&[], &[], &[], &[]).is_ok()); // an empty batch
+    }
 }

@@ -271,6 +271,7 @@ def main():
     eb.record(lstreams[0])
     barrier()
     launch_ms_alone = ea.elapsed_time(eb)
+    kernel_ms_local, elapsed_local, launch_alone_local = kernel_ms, elapsed, launch_ms_alone
     elapsed, kernel_ms, launch_ms_alone = reduce([elapsed, kernel_ms, launch_ms_alone],
                                                  dist.ReduceOp.MAX if use_dist else None)
 
@@ -280,6 +281,9 @@ def main():
     used = used[: min(2, max(1, args.steps + args.warmup))]
     match = min(float((full == -1).float().mean().item()) for full in used)
     match = reduce([match], dist.ReduceOp.MIN)[0] if use_dist else match
+
+    multi = multi_gpu_diagnostics(args, v, barrier, dist, torch, lstreams, ptrs, n, L, words, d_vers, d_alls, world,
+                                  kernel_ms_local, elapsed_local, launch_alone_local) if use_dist else None
 
     e2e = host_path(args, v, verify, barrier, reduce, dist, torch, dev, lstreams, d_pk, d_sig, d_msg, d_off, d_vers,
                     d_alls, n, L, words, use_dist, world) if args.e2e else None
@@ -354,6 +358,8 @@ def main():
         }
         if e2e:
             out.update(e2e)
+        if multi:
+            out["multi_gpu"] = multi
     if rank == 0 and world == 1 and args.traffic_leg and not args.senders and not use_dist:
         out["at2_traffic"] = at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -422,6 +428,43 @@ def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
                       "verify by comb additions (DESIGN §10d); combs built in the warm-up"}
 
 
+def multi_gpu_diagnostics(args, v, barrier, dist, torch, lstreams, ptrs, n, L, words, d_vers, d_alls, world,
+                          kernel_ms, elapsed, launch_alone):
+    """N > 1 (and the world-1 torchrun rehearsal): what a sub-linear scaling curve needs to be read.
+    Per rank: the timed region's device time per step (verify + all-gather, `kernel_ms`), its wall time, one launch
+    alone, then two extra measurements on the same launch stream with HIP events: verify-only steps (the rank's shard,
+    no collective) and gather-only steps (an empty shard: the slice zeroing + the RCCL all-gather of `words` words per
+    rank), so kernel time, collective time and a slow rank separate. All gathered to rank 0 over gloo."""
+    steps = max(2, args.steps)
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier()
+        e0.record(lstreams[0])
+        for _ in range(steps):
+            fn()
+        e1.record(lstreams[0])
+        barrier()
+        return e0.elapsed_time(e1) / steps
+
+    s0 = lstreams[0].cuda_stream
+    verify_ms = timed(lambda: v.verify_batch_device(*ptrs[:3], n * L, ptrs[3], n, d_vers[0].data_ptr(), s0))
+    gather_ms = timed(lambda: v.verify_shard_gather_device(0, 0, 0, 0, 0, 0, words, d_alls[0].data_ptr(), s0))
+    mine = torch.tensor([kernel_ms, elapsed, launch_alone, verify_ms, gather_ms], dtype=torch.float64)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    per = [r.tolist() for r in allr]
+    col = lambda j: [p[j] for p in per]  # noqa: E731
+    km = col(0)
+    return {"ranks": world, "kernel_ms_per_rank": km, "kernel_ms_min": min(km), "kernel_ms_max": max(km),
+            "max_rank": int(max(range(world), key=lambda r: km[r])), "elapsed_s_per_rank": col(1),
+            "launch_ms_alone_per_rank": col(2), "verify_only_ms_per_rank": col(3), "gather_only_ms_per_rank": col(4),
+            "gather_words_per_rank": words, "gather_bytes_per_step": 4 * words * world,
+            "method": "per-rank HIP events on launch stream 0: kernel_ms = the timed region (verify + RCCL all-gather per "
+                      "step, two streams); verify_only = the rank's shard without the collective; gather_only = "
+                      f"at2v_verify_shard_gather_device with an empty shard ({steps} steps each); gathered over gloo"}
+
+
 def dry_run(args, rank, world, use_dist, dist, torch, np):
     """CPU rehearsal of the multi-rank bench (tests/test_bench_launch.py): the same launcher, env and gloo control
     plane; each rank's verdict words come from the oracle over its index shard of a small node batch and are
@@ -440,18 +483,32 @@ def dry_run(args, rank, world, use_dist, dist, torch, np):
     lo, hi = at2dist.shard_bounds(n, world)[rank]
     per = at2dist.padded_words_per_rank(n, world)
     bits = np.zeros(per * 32, np.uint8)
+    t0 = time.perf_counter()
     if hi > lo:
         bits[: hi - lo] = o.verify_batch(pk[lo:hi], sig[lo:hi], msg, off[lo:hi + 1], 0, 2)
+    verify_ms = (time.perf_counter() - t0) * 1e3
     local = torch.from_numpy(np.packbits(bits, bitorder="little").view(np.int32).copy())
+    t0 = time.perf_counter()
     full = at2dist.gather_verdicts(local, world) if use_dist else local
+    gather_ms = (time.perf_counter() - t0) * 1e3
     got = at2dist.node_bitmap_from_shards(full, n, world)
     match = float((got == want).mean())
     t = torch.tensor([match, float(uid[0] == bytes(range(128)))], dtype=torch.float64)
     if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         dist.barrier()
-    return {"dry_run": True, "n_gpus": world, "records": n, "verdict_match": t[0].item(),
-            "unique_id_shared": bool(t[1].item()), "valid": int(want.sum())}
+    out = {"dry_run": True, "n_gpus": world, "records": n, "verdict_match": t[0].item(),
+           "unique_id_shared": bool(t[1].item()), "valid": int(want.sum())}
+    if use_dist:  # the multi_gpu keys of the GPU line, from the CPU stand-ins (oracle verify, gloo gather)
+        mine = torch.tensor([verify_ms + gather_ms, verify_ms, gather_ms], dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        km = [r[0].item() for r in allr]
+        out["multi_gpu"] = {"ranks": world, "kernel_ms_per_rank": km, "kernel_ms_min": min(km), "kernel_ms_max": max(km),
+                            "max_rank": int(max(range(world), key=lambda r: km[r])),
+                            "verify_only_ms_per_rank": [r[1].item() for r in allr],
+                            "gather_only_ms_per_rank": [r[2].item() for r in allr], "gather_words_per_rank": per}
+    return out
 
 
 def host_path(args, v, verify, barrier, reduce, dist, torch, dev, lstreams, d_pk, d_sig, d_msg, d_off, d_vers, d_alls,

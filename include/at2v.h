@@ -26,11 +26,12 @@ extern "C" {
 #endif
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
- * version 4 appended at2v_opts.sender_comb and the AT2V_QUEUE_SENDER_COMB queue flag; version 3 appended
- * at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
+ * version 5 appended at2v_queue_opts.sender_cache and at2v_info.cache_capacity / cache_claims / cache_evicted /
+ * cache_compactions (the sender cache replaces entries instead of restarting empty); version 4 appended
+ * at2v_opts.sender_comb and the AT2V_QUEUE_SENDER_COMB queue flag; version 3 appended at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
  * at2v_opts.small_batch_max and at2v_queue_opts.flags). A binding checks at2v_abi_version() == AT2V_ABI_VERSION
  * before passing any struct (the Python and Rust bindings in this repo refuse a mismatching library). */
-#define AT2V_ABI_VERSION 4
+#define AT2V_ABI_VERSION 5
 int at2v_abi_version(void);
 
 typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, and the RCCL
@@ -48,9 +49,12 @@ typedef struct {
   uint32_t small_batch_max; /* launches of at most this many records run the low-latency kernel (two lanes per
                                record, one wave per SIMD); 0 = 32768; AT2V_SMALL_BATCH_OFF = never */
   uint32_t sender_cache;    /* per-sender A cache (AT2 senders repeat: accounts/account.rs:36-43): capacity in distinct
-                               public keys, 0 = off. When full it is cleared and refilled. A record whose sender A is cached skips decoding A and building
+                               public keys, 0 = off. A record whose sender A is cached skips decoding A and building
                                its [j]A table; the verdict is unchanged (the cache holds only values derived from the
-                               32 bytes of A, and every hit is confirmed by comparing those bytes). */
+                               32 bytes of A, and every hit is confirmed by comparing those bytes). A key seen for the
+                               first time is verified without the cache; its entry is built on the context's build
+                               stream after that launch and serves later launches. When the capacity is reached, the
+                               least recently used entries (by launch) are replaced; up to 3/4 of the capacity stays. */
   uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(10i)](-A), 2.1 MB
                                per key, sender_cache x 2.1 MB per device, plus a 67 MB comb of B per context), and a
                                64-record chunk whose senders are all cached is verified by 42 table additions and one
@@ -74,10 +78,9 @@ enum {
 
 /* Create / destroy a context. opts may be NULL (device 0, one GPU, DALEK_V1). Replaces nothing in the
  * reference directly: it owns what drop's SystemManager::run(.., num_cpus::get()) workers did
- * implicitly (rpc.rs:124-125). A context is not thread-safe: one thread at a time. Its verify launches take
- * turns on the device scratch in call order, whatever streams they are given (each launch waits for the
- * previous one of the same context), so launches on different streams never overlap; use one context per
- * concurrent verifier. */
+ * implicitly (rpc.rs:124-125). A context is not thread-safe: one thread at a time. A device has two scratch sets that
+ * its verify launches take in turn, whatever streams they are given: a launch waits (on the device) for the launch that
+ * last used its set, so launches on two streams overlap by up to one launch and launches on one stream are ordered. */
 int at2v_create(const at2v_opts* opts, at2v_ctx** out);
 void at2v_destroy(at2v_ctx* ctx);
 
@@ -152,7 +155,13 @@ typedef struct {
   uint64_t cache_entries;    /* at2v_opts.sender_cache: distinct senders now cached (all devices) */
   uint64_t cache_chunks;     /* 64-record chunks verified with the cache on */
   uint64_t cache_chunk_hits; /* ... of which every record's A came from the cache (A decode and [j]A skipped) */
+  uint64_t cache_capacity;   /* keys the cache can hold (all devices) */
+  uint64_t cache_claims;     /* keys claimed (first seen, or seen again after being replaced) */
+  uint64_t cache_evicted;    /* entries replaced to make room */
+  uint64_t cache_compactions;/* replacement passes */
 } at2v_info;
+/* With a sender cache, at2v_get_info first waits for the context's cache work (its build stream, which follows every
+ * cached launch and therefore waits for those launches, and whatever each launch's stream ran before them). */
 int at2v_get_info(at2v_ctx* ctx, at2v_info* out);
 
 /* ---- multi-GPU, one process per GPU: RCCL all-gather of the verdict bitmap ----
@@ -206,9 +215,11 @@ typedef struct {
   uint32_t depth;         /* batch slots, >= 2; 0 = 3 */
   uint32_t flags;         /* AT2V_QUEUE_EAGER: also seal whenever no batch is in flight; AT2V_QUEUE_SENDER_COMB:
                              per-sender combs (at2v_opts.sender_comb) */
+  uint32_t sender_cache;  /* with AT2V_QUEUE_SENDER_COMB: keys the queue's context caches (at2v_opts.sender_cache,
+                             2.1 MB of HBM each); 0 = 1024 */
 } at2v_queue_opts;
 #define AT2V_QUEUE_EAGER 1u
-#define AT2V_QUEUE_SENDER_COMB 2u /* the queue's context gets sender_cache = 1024 keys with sender_comb = 1 */
+#define AT2V_QUEUE_SENDER_COMB 2u /* the queue's context gets a sender cache (sender_cache keys) with sender_comb = 1 */
 typedef struct {
   uint64_t submitted, completed, batches, failed_batches;
   double mean_batch;           /* records per completed batch */

@@ -172,7 +172,8 @@ int main(int argc, char** argv) {
   size_t bad_d = 0, bad_s = 0;
   int limit = argc > 2 ? atoi(argv[2]) : (int)n;
   // 1: the half-size equation (verify_half); 2: on the unsigned field; 3: two lanes per signature (verify_pair_part);
-  // 4: from per-key combs (verify_comb_fu, the sender-comb path); 5: the comb path's low-latency four-wave split
+  // 4: from per-key combs (verify_comb_fu, the sender-comb path); 5: the comb path's low-latency four-wave split;
+  // 6: the four-wave kernel's split half-size check for chunks without combs (split_* in at2v_verify_fu.h)
   const int half = argc > 3 ? atoi(argv[3]) : 0;
   std::map<std::vector<uint32_t>, HostComb> combs;
   HostBComb bcomb;
@@ -191,7 +192,26 @@ int main(int argc, char** argv) {
     static HostTabB16 tb;
     HostTabA ta, tr;
     int d, s;
-    if (half == 5) {  // the low-latency kernel's four-way split (comb_decode_r | B sum | A sums) and comb_check_split
+    if (half == 6) {  // wave 0 | wave 1 | wave 2, then the two ladders, -[t]B from the comb of B, and the combine
+      auto split = [&](int policy) {
+        HostTabAFu fa, fr;
+        gu_p3 Ad, P0, P1;
+        const int ok0 = split_a_side(Ad, R, A, S, policy, fa);
+        const int ok1 = split_r_side(R, fr);
+        uint32_t c0d[8], c1d[8], td[8];
+        int c1_neg, nw;
+        const int ok2 = split_scalars(c0d, c1d, td, c1_neg, nw, R, A, S, len, mw);
+        nw = nw < 1 ? 1 : nw;  // (the kernel takes the wave maximum; one lane here)
+        split_side_ladder(P0, c0d, nw, 0, fa);
+        split_side_ladder(P1, c1d, nw, c1_neg, fr);
+        gu_cached c1, ntb;
+        gu_p3_to_cached(c1, P1);
+        split_neg_tb(ntb, td, bcomb);
+        return ok0 & ok1 & ok2 & split_combine(P0, c1, ntb);
+      };
+      d = split(POLICY_DALEK_V1);
+      s = split(POLICY_LIBSODIUM_1_0_18);
+    } else if (half == 5) {  // the low-latency kernel's four-way split (comb_decode_r | B sum | A sums) and comb_check_split
       std::vector<uint32_t> key(A, A + 8);
       auto it = combs.find(key);
       if (it == combs.end()) it = combs.try_emplace(key, A).first;

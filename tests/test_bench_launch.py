@@ -24,6 +24,13 @@ def test_bench_self_launch_dry_run(gpus):
     r = json.loads(lines[0])
     assert r["dry_run"] and r["n_gpus"] == gpus and r["verdict_match"] == 1.0 and r["unique_id_shared"]
     assert 0 < r["valid"] < r["records"]
+    # the N > 1 line separates per-rank kernel time, collective time and the slowest rank
+    m = r["multi_gpu"]
+    for k in ("kernel_ms_per_rank", "verify_only_ms_per_rank", "gather_only_ms_per_rank"):
+        assert len(m[k]) == gpus and all(x >= 0 for x in m[k]), k
+    assert m["ranks"] == gpus and 0 <= m["max_rank"] < gpus
+    assert m["kernel_ms_max"] == max(m["kernel_ms_per_rank"]) == m["kernel_ms_per_rank"][m["max_rank"]]
+    assert m["kernel_ms_min"] <= m["kernel_ms_max"] and m["gather_words_per_rank"] > 0
 
 
 @pytest.mark.parametrize("fail_rank", [1, 0])

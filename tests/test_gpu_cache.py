@@ -4,10 +4,12 @@ AT2 senders issue consecutive sequences (/root/reference/src/bin/server/accounts
 payloads of a node batch (client.rs:77-78). With the cache on, a wave whose 64 records all find their A in the cache
 (fingerprint nominates an entry, then all 32 key bytes are compared) skips decoding A and building [j]A. The verdict
 must stay a pure function of (A, R||S, M): every test here compares with the oracle or the golden fixtures, through
-the C ABI, in every cache state — entry built in the same launch, warm, fingerprint collisions (forced with
-AT2V_TEST_CACHE_FP_BITS), cache full (restart), undecodable / small-order / non-canonical senders cached together with
-their decode verdict, and both policies. Every test runs twice: with the [j]A tables (sender_comb off) and with per-key
-combs (sender_comb on: all-hit chunks verify by table additions only, at2v_comb.h)."""
+the C ABI, in every cache state — key claimed in this launch (entry still being built on the build stream: the launch
+verifies it without the cache), warm, fingerprint collisions (forced with AT2V_TEST_CACHE_FP_BITS), cache full
+(compaction: the least recently used entries are replaced), undecodable / small-order / non-canonical senders cached
+together with their decode verdict, and both policies. Every test runs twice: with the [j]A tables (sender_comb off) and
+with per-key combs (sender_comb on: all-hit chunks verify by table additions only, at2v_comb.h). `v.info()` waits for the
+context's build stream, so a launch after it finds every key claimed before it built and valid."""
 import os
 
 import numpy as np
@@ -34,11 +36,12 @@ def at2v_mod():
     return at2v
 
 
-def _mutate(pk, sig, msg, off, rng, k):
-    """k records mutated in R, S, M or A (a bit flip): each then has exactly one verdict the oracle decides"""
+def _mutate(pk, sig, msg, off, rng, k, kinds=4):
+    """k records mutated in R, S, M or A (a bit flip; kinds=3: never A): each then has exactly one verdict the oracle
+    decides"""
     pk, sig, msg = pk.copy(), sig.copy(), msg.copy()
     for i in rng.choice(len(pk), k, replace=False):
-        kind = rng.integers(0, 4)
+        kind = rng.integers(0, kinds)
         if kind == 0:
             sig[i, rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
         elif kind == 1:
@@ -60,14 +63,17 @@ def test_config1_traffic_every_chunk_hits(at2v_mod, oracle, comb):
     want2 = oracle.verify_batch(pk2, sig2, msg2, off)
     assert want.all() and 0 < want2.sum() < len(want2)
     with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=comb) as v:
-        for rep in range(2):
-            assert np.array_equal(v.verify_batch(pk, sig, msg, off), want)
+        assert np.array_equal(v.verify_batch(pk, sig, msg, off), want)  # claims the 64 senders, verified uncached
+        info = v.info()  # (waits for the build stream: the 64 entries are built and valid)
+        assert info["cache_entries"] == 64 and info["cache_claims"] == 64
+        assert info["cache_chunks"] == 64 and info["cache_chunk_hits"] == 0
+        assert np.array_equal(v.verify_batch(pk, sig, msg, off), want)  # every chunk from the cache
         info = v.info()
-        assert info["cache_entries"] == 64
-        assert info["cache_chunks"] == 2 * 64 and info["cache_chunk_hits"] == info["cache_chunks"]
+        assert info["cache_chunks"] == 2 * 64 and info["cache_chunk_hits"] == 64
         got2 = v.verify_batch(pk2, sig2, msg2, off)  # mutated A's are new keys: new entries, some undecodable
         assert np.array_equal(got2, want2), np.nonzero(got2 != want2)[0][:10]
         assert v.info()["cache_entries"] > 64
+        assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want2)  # ... now cached, undecodable ones too
 
 
 @pytest.mark.parametrize("policy", ["dalek", "libsodium"])
@@ -82,6 +88,7 @@ def test_golden_sets_with_cache(at2v_mod, golden, policy, comb):
             for rep in range(2):
                 got = v.verify_batch(g.pk, g.sig, g.msg, g.off)
                 assert np.array_equal(got, want), (name, rep, np.nonzero(got != want)[0][:10])
+                v.info()  # the next pass finds this pass's keys built
 
 
 def test_repeated_adversarial_senders(at2v_mod, oracle, comb):
@@ -96,9 +103,11 @@ def test_repeated_adversarial_senders(at2v_mod, oracle, comb):
     pk_t, sig_t, msg_t = _mutate(pk_t, sig_t, msg_t, off_t, np.random.default_rng(5), 1500)
     want = oracle.verify_batch(pk_t, sig_t, msg_t, off_t)
     with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=4096, sender_comb=comb) as v:
-        for rep in range(2):
+        for rep in range(3):
             got = v.verify_batch(pk_t, sig_t, msg_t, off_t)
-            assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+            assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
+            if rep == 1:
+                v.info()
 
 
 def test_fingerprint_collisions_fall_back(at2v_mod, oracle, monkeypatch, comb):
@@ -109,24 +118,78 @@ def test_fingerprint_collisions_fall_back(at2v_mod, oracle, monkeypatch, comb):
     pk2, sig2, msg2 = _mutate(pk, sig, msg, off, np.random.default_rng(7), 200)
     want = oracle.verify_batch(pk2, sig2, msg2, off)
     with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=comb) as v:
-        for rep in range(2):
+        for rep in range(3):
             assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want)
+            v.info()
         info = v.info()
         assert info["cache_entries"] <= 4 and info["cache_chunk_hits"] < info["cache_chunks"]
 
 
-def test_cache_full_restarts(at2v_mod, oracle, comb):
-    """capacity 16 < 64 senders: the first launch fills the cache (the rest go uncached), a later launch starts over;
-    verdicts exact throughout. Claims beyond the capacity keep their tags but are never built (invalid entries)."""
+def test_cache_full_compacts(at2v_mod, oracle, comb):
+    """capacity 16 < 64 senders: the first launch hands out all 16 payloads (the other claims stay without one), so
+    the cache is compacted before a later launch (at most 3/4 of the entries stay, the least recently used go back to
+    the free list); verdicts exact throughout, the cache never holds more than its capacity."""
     pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
     pk2, sig2, msg2 = _mutate(pk, sig, msg, off, np.random.default_rng(9), 100)
     want = oracle.verify_batch(pk2, sig2, msg2, off)
     with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=16, sender_comb=comb) as v:
-        for rep in range(4):
+        for rep in range(5):
             assert np.array_equal(v.verify_batch(pk2, sig2, msg2, off), want), rep
             assert v.info()["cache_entries"] <= 16
         info = v.info()
-        assert info["cache_chunk_hits"] < info["cache_chunks"]  # some waves had a sender left out
+        assert info["cache_chunk_hits"] < info["cache_chunks"]  # waves had senders left out
+        assert info["cache_compactions"] >= 1 and info["cache_evicted"] >= 1 and info["cache_capacity"] == 16, info
+
+
+def _gen_senders(at2v_mod, n, L, senders):
+    """n valid records (GPU generator), record i signed by sender i % senders, as host arrays"""
+    import torch
+    dev = "cuda:0"
+    d_pk = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    d_sig = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+    d_msg = torch.zeros(n * L, dtype=torch.uint8, device=dev)
+    d_off = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    with at2v_mod.BatchVerifier() as g:
+        g.gen_records_device(CFG_SEED, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream, senders=senders)
+        torch.cuda.synchronize()
+    return (d_pk.cpu().numpy().reshape(n, 32), d_sig.cpu().numpy().reshape(n, 64), d_msg.cpu().numpy(),
+            d_off.cpu().numpy().astype(np.uint32))
+
+
+def test_senders_4x_capacity(at2v_mod, oracle, comb):
+    """VERDICT r3 "Next" 5: 4x more senders than the cache holds. 256 senders, capacity 64; launch k carries the 1024
+    records (16 per sender, 4 senders per 64-record chunk) of the 64 senders in a window that slides by 16 senders per
+    launch over the 256, mutated, so
+    a quarter of the working set changes every launch and the whole sender set cycles through the cache 3 times.
+    Verdicts equal the oracle's in every launch; the cache compacts (least recently used entries replaced) instead of
+    restarting empty, it never holds more than 64 keys, and the senders still in the window hit (hit rate printed)."""
+    S, L = 256, 48
+    pk, sig, msg, off = _gen_senders(at2v_mod, S * 16, L, S)
+    snd = np.arange(S * 16) % S
+    rng = np.random.default_rng(17)
+    hits, chunks = [], []
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=64, sender_comb=comb) as v:
+        for launch in range(12):
+            window = set(((np.arange(64) + 16 * launch) % S).tolist())
+            # grouped by sender (a 64-record chunk holds 4 senders), so chunks of cached senders hit
+            idx = np.array(sorted((i for i in range(S * 16) if snd[i] in window), key=lambda i: (snd[i], i)))
+            p2, s2 = pk[idx], sig[idx]
+            m2 = np.concatenate([msg[off[i]:off[i + 1]] for i in idx])
+            o2 = (np.arange(len(idx) + 1) * L).astype(np.uint32)
+            p2, s2, m2 = _mutate(p2, s2, m2, o2, rng, 40, kinds=3)  # (a mutated A is one more sender)
+            want = oracle.verify_batch(p2, s2, m2, o2)
+            h0 = v.info()
+            got = v.verify_batch(p2, s2, m2, o2)
+            assert np.array_equal(got, want), (launch, np.nonzero(got != want)[0][:10])
+            h1 = v.info()
+            hits.append(h1["cache_chunk_hits"] - h0["cache_chunk_hits"])
+            chunks.append(h1["cache_chunks"] - h0["cache_chunks"])
+            assert h1["cache_entries"] <= 64
+        info = v.info()
+        print(f"4x senders: chunk hit rate {sum(hits)}/{sum(chunks)}, per launch {hits}; {info}")
+        assert info["cache_compactions"] >= 2 and info["cache_evicted"] >= 64, info
+        assert sum(hits) > 0, hits
 
 
 def test_generator_with_repeating_senders(at2v_mod, oracle):
@@ -190,11 +253,15 @@ def test_golden_sets_comb_lat_kernel(at2v_mod, golden, policy):
             g = golden[name]
             want = g.dalek if policy == "dalek" else g.sodium
             for rep in range(2):
+                h0 = v.info()  # (the second pass finds the first pass's keys built)
                 got = np.concatenate([_verify_slice(v, g, a, b) for a, b in _slices(g.n, rng)])
                 assert np.array_equal(got, want), (name, rep, np.nonzero(got != want)[0][:10])
-        info = v.info()
-        # every chunk took the comb branch of the four-wave kernel (none fell back to wave 0's ladder)
-        assert info["cache_chunks"] > 0 and info["cache_chunk_hits"] == info["cache_chunks"], info
+                h1 = v.info()
+                chunks, hits = h1["cache_chunks"] - h0["cache_chunks"], h1["cache_chunk_hits"] - h0["cache_chunk_hits"]
+                if rep == 0:  # cold: a chunk with a key not seen before runs the two-wave half-size split
+                    assert hits < chunks, (name, h1)
+                else:  # warm: every chunk takes the comb branch of the four-wave kernel
+                    assert chunks > 0 and hits == chunks, (name, h1)
 
 
 def test_comb_lat_kernel_mixed_hit_and_fallback_chunks(at2v_mod, oracle, golden):
@@ -227,7 +294,7 @@ def test_comb_lat_kernel_mixed_hit_and_fallback_chunks(at2v_mod, oracle, golden)
     # capacity 96: the 64 cfg1 senders fit, most adversarial keys do not (their chunks fall back)
     with at2v_mod.BatchVerifier(sender_cache=96, sender_comb=True) as v:
         assert np.array_equal(v.verify_batch(pk, sig, msg, off), oracle.verify_batch(pk, sig, msg, off))  # warm
-        h0 = v.info()
+        h0 = v.info()  # (waits for the 64 senders' combs)
         for rep in range(3):
             got = v.verify_batch(P, S, M, O)
             assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
@@ -254,5 +321,5 @@ def test_comb_small_and_ragged_launches(at2v_mod, oracle, n):
         for rep in range(2):
             got = v.verify_batch(pk, sig, msg, off)
             assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
-        info = v.info()
+            info = v.info()
         assert info["cache_chunk_hits"] > 0

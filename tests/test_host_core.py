@@ -41,9 +41,9 @@ def host_exe_asan(host_exes):
     return host_exes[1]
 
 
-MODES = [0, 1, 2, 3, 4, 5]
+MODES = [0, 1, 2, 3, 4, 5, 6]
 MODE_IDS = ["full_length", "half_size", "half_size_unsigned_field", "two_lanes_per_record", "sender_comb",
-            "sender_comb_split"]
+            "sender_comb_split", "four_wave_split_half_size"]
 
 
 @pytest.mark.parametrize("half", MODES, ids=MODE_IDS)

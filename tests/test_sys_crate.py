@@ -246,3 +246,18 @@ def test_safe_layer_checks_abi_version():
         body = src[src.index(ctor):]
         body = body[:body.index("\n}\n")]
         assert "check_abi()?" in body, ctor
+
+
+def test_safe_wrappers_check_offsets_against_msg():
+    """ADVICE r3 (medium): the safe BatchVerifier::verify and Queue::submit hand msg.as_ptr() to C functions that read
+    message bytes up to msg_off[n] with no length argument. Both must go through check_records, which refuses
+    decreasing offsets and msg_off[n] > msg.len() (a #[test] in the crate covers it; no cargo here, so textually)."""
+    src = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    fn = src[src.index("fn check_records("):]
+    fn = fn[:fn.index("\n}\n")]
+    assert "w[1] < w[0]" in fn and "msg.len()" in fn
+    for wrapper in ("pub fn verify(", "pub fn submit("):
+        body = src[src.index(wrapper):]
+        body = body[:body.index("\n    }\n")]
+        assert "check_records(pk, sig, msg, msg_off)?" in body, wrapper
+    assert "fn safe_layer_rejects_offsets_outside_msg" in src and "&[0, 5]" in src

@@ -1,0 +1,65 @@
+#!/bin/bash
+# gpu_run.sh — the GPU-box recipe (runs ON the box, from the repo root, under gpurun):
+#   tools/gpu.sh 900 'bash tools/gpu_run.sh <tag> <stage> [<stage> ...]'
+# Stages run in the order given; each has its own time limit, and the first failing stage ends the run (no GPU step
+# after a failure). Outputs go to gpurun_out/<tag>/ (copy what is to be kept into profiles/<tag>/).
+#   suite         pytest -m gpu (the whole parity / boundary / cache suite)
+#   tests=<expr>  pytest -m gpu -k <expr>
+#   files=<a,b>   pytest -m gpu on those test files
+#   smoke         __graft_entry__.smoke()
+#   bench         python bench.py (the default driver line: config 2 + at2_traffic + roofline + cpu_baseline)
+#   bench1        python bench.py with the PMC passes and CPU baseline off (a quick rate check)
+#   torchrun1     the world-1 torchrun rehearsal of the N > 1 bench path (RCCL gather inside the timed loop)
+#   rocprof       rocprofv3 --kernel-trace --stats of a bench run with one scratch set (per-kernel averages)
+#   latency       tools/latency_probe.py --comb 1 (small-batch and first-seen-sender latency)
+#   fresh         tools/fresh_sweep.sh: config 5 with a stream of first-seen senders (queue p50/p99 per node)
+#   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
+#   ab=<a,b,...>  tools/ab_bench.py over at2-node_amd/at2v/variants/libat2v_<a>.so ... (distinct keys)
+#   abcomb=<...>  the same on 64-sender traffic with combs
+set -o pipefail
+TAG=$1; shift
+D=gpurun_out/$TAG
+mkdir -p $D
+export TMPDIR=/tmp
+run() {  # run <name> <seconds> <cmd...>: stdout+stderr to $D/<name>.txt, tail on failure
+  local name=$1 t=$2; shift 2
+  echo "[gpu_run] $name ($t s): $*"
+  timeout -k 10 "$t" "$@" > "$D/$name.txt" 2>&1 || { echo "[gpu_run] $name FAILED rc=$?"; tail -40 "$D/$name.txt"; exit 1; }
+  tail -3 "$D/$name.txt"
+}
+for st in "$@"; do
+  case "$st" in
+    suite) run gpu_tests 1100 python -u -m pytest tests -m gpu -v --maxfail=3 --timeout 300 --timeout-method thread
+           cp gpurun_out/config5_*.json $D/ 2>/dev/null ;;
+    files=*) run gpu_tests_f 900 python -u -m pytest $(echo "${st#files=}" | tr ',' ' ') -m gpu -v -x --timeout 300 \
+               --timeout-method thread
+             cp gpurun_out/config5_*.json $D/ 2>/dev/null ;;
+    tests=*) run gpu_tests_k 900 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread -k "${st#tests=}"
+             cp gpurun_out/config5_*.json $D/ 2>/dev/null ;;
+    smoke) run smoke 180 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 500 python3 bench.py
+           grep '^{' $D/bench.txt > $D/bench.json ;;
+    bench1) run bench1 300 python3 bench.py --pmc-traffic 0 --cpu-sample 0 --e2e 0
+            grep '^{' $D/bench1.txt > $D/bench1.json ;;
+    torchrun1) run torchrun1 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+                 --master-port 29533 bench.py --gpus 1 --steps 10 --warmup 2 --e2e 0
+               grep '^{' $D/torchrun1.txt > $D/torchrun1.json ;;
+    rocprof) export AT2V_SCRATCH_SETS=1
+             run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- \
+               python3 bench.py --steps 20 --warmup 3 --pmc-traffic 0 --cpu-sample 0 --e2e 0
+             unset AT2V_SCRATCH_SETS
+             find $D/prof -name '*kernel_stats.csv' -exec cp {} $D/kernel_stats.csv \; ;;
+    fresh) run fresh 900 bash tools/fresh_sweep.sh $TAG ;;
+    pmc) run pmc 1100 bash tools/profile.sh $TAG ;;
+    latency) run latency 400 python3 tools/latency_probe.py --reps 100 --comb 1
+             grep '^{' $D/latency.txt > $D/latency_comb1.json ;;
+    ab=*) libs=""
+          for v in $(echo "${st#ab=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
+          run ab 900 python3 tools/ab_bench.py $libs --rounds 12 ;;
+    abcomb=*) libs=""
+          for v in $(echo "${st#abcomb=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
+          run abcomb 900 python3 tools/ab_bench.py $libs --rounds 12 --senders 64 --comb ;;
+    *) echo "[gpu_run] unknown stage $st"; exit 2 ;;
+  esac
+done
+echo "[gpu_run] done: $D"

@@ -7,8 +7,12 @@ For batches of B records (default 1, 20, 64, 1024), each measured `--reps` times
   sync     : wall time of at2v_verify_batch (host arrays: H2D, kernel, D2H, synchronise);
   queue    : wall time from at2v_queue_submit of the B records to the last verdict polled (eager queue, idle,
              one batch in flight at a time);
+  fresh    : (--comb 1) device time of launches whose B keys the context has never seen (steady state of a stream of
+             first-seen senders: the in-kernel lookup, then the two-wave half-size split);
   first    : (--comb 1) device time of the FIRST launch of the B records in a fresh context, whose B keys are new:
-             the cache lookup, one comb build per new key, then the verify (the cost a first-seen sender pays once);
+             the in-kernel lookup claims them and their chunks run the two-wave half-size split (the cost a first-seen
+             sender pays once; its comb is built afterwards on the context's build stream: `first_combs_ready_us` is
+             the wall time from that launch until at2v_get_info, which waits for the build stream, returns);
 reports p50/p90 per stage as JSON. Records come from the oracle generator (all valid), checked once per size."""
 import argparse
 import json
@@ -33,6 +37,8 @@ def main():
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--msg-len", type=int, default=48)
     ap.add_argument("--comb", type=int, default=0, help="1 = per-sender combs (the keys are cached after the first rep)")
+    ap.add_argument("--fresh-reps", type=int, default=20,
+                    help="(--comb 1) launches of B records with keys the context has not seen (fresh_keys_launch)")
     a = ap.parse_args()
     import torch
 
@@ -60,16 +66,42 @@ def main():
         first_us = None
         if a.comb:
             vc = at2v.BatchVerifier(device=0, sender_cache=1024, sender_comb=True)
+            # a running node's context: one earlier launch (other keys) before the measured one, so the measurement is
+            # the first payload of new senders, not the first launch of a new context (that costs ~0.7 ms more, once)
+            wp, wg, wm, wf = o.gen_records(0x4154325F, 1 << 30, 64, a.msg_len)
+            assert vc.verify_batch(wp, wg, wm, wf).all()
+            vc.info()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t_first = time.perf_counter()
             e0.record(s)
             vc.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), int(f[-1]), d_off.data_ptr(),
                                    B, d_ver.data_ptr(), s.cuda_stream)
             e1.record(s)
+            vc.info()  # waits for the build stream (combs of the B new keys)
+            combs_ready_us = (time.perf_counter() - t_first) * 1e6
             torch.cuda.synchronize()
             first_us = e0.elapsed_time(e1) * 1e3
             assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
             vc.close()
+        fresh = []
+        if a.comb and a.fresh_reps:
+            # steady state of first-seen senders: every rep launches B records whose keys the context has not seen
+            fp, fg, fm, ff = o.gen_records(0x4154325F, 1 << 24, B * a.fresh_reps, a.msg_len)
+            dd = [torch.from_numpy(x.reshape(-1).copy()).cuda() for x in (fp, fg)]
+            dm = torch.from_numpy(np.concatenate([fm, np.zeros(16, np.uint8)])).cuda()
+            for r in range(a.fresh_reps):
+                lo = r * B
+                d_off2 = torch.from_numpy((ff[lo:lo + B + 1] - ff[lo]).view(np.int32).copy()).cuda()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                v.verify_batch_device(dd[0].data_ptr() + lo * 32, dd[1].data_ptr() + lo * 64, dm.data_ptr() + int(ff[lo]),
+                                      int(ff[lo + B] - ff[lo]), d_off2.data_ptr(), B, d_ver.data_ptr(), s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
+                if r >= 2:
+                    fresh.append(e0.elapsed_time(e1) * 1e3)
         kern, sync, queue = [], [], []
         for r in range(a.reps + 5):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -94,8 +126,11 @@ def main():
         assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
         out["sizes"][B] = {k: {"p50_us": pct(x, 50), "p90_us": pct(x, 90)} for k, x in
                            (("kernel", kern), ("sync", sync), ("queue", queue))}
+        if fresh:
+            out["sizes"][B]["fresh_keys_launch"] = {"p50_us": pct(fresh, 50), "p90_us": pct(fresh, 90)}
         if first_us is not None:
             out["sizes"][B]["first_launch_new_keys_us"] = first_us
+            out["sizes"][B]["first_combs_ready_us"] = combs_ready_us
         print(B, json.dumps(out["sizes"][B]), file=sys.stderr)
     q.close()
     v.close()

@@ -23,6 +23,7 @@ import hashlib
 import json
 import multiprocessing as mp
 import os
+import queue as queue_mod
 import sys
 import threading
 import time
@@ -37,7 +38,7 @@ def node_main(idx, inboxes, result_q, args, total):
     from at2v.node import VERDICT_FAILED, IngestQueue, Ledger, SendAssetRequest, pack_send_asset, verdict_mask
 
     q = IngestQueue(device=0, max_batch=args.batch, max_delay_us=args.delay_us, max_msg_bytes=48, depth=3,
-                    eager=args.eager, sender_comb=bool(args.comb))
+                    eager=args.eager, sender_comb=bool(args.comb), sender_cache=args.cache)
     led = Ledger()
     lock = threading.Lock()
     chunks = []  # submitted runs, ticket order: [first, pk, seq, rcp, amt, t_arrival]
@@ -186,7 +187,28 @@ def client_main(inboxes, ready_q, args):
         forged[50] ^= 0x08
         reqs.insert(int(j) + 1, (reqs[j][0], reqs[j][1], reqs[j][2], reqs[j][3] + 1, wire_signature(bytes(forged))))
     total = len(reqs)
-    ready_q.put({"keys": [pks[i].tobytes() for i in range(args.senders)], "total": total, "bad": nbad})
+    # a stream of first-seen senders (--fresh-frac): each fresh key sends one transfer (sequence 1) to a regular
+    # sender, spread evenly through the run; on every node its first payload finds no cache entry
+    fresh_keys = []
+    nfresh = int(total * args.fresh_frac)  # (after the forgeries: they index the regular arrays)
+    if nfresh:
+        vf = at2v.BatchVerifier(device=0)
+        fseeds = rng.integers(0, 256, (nfresh, 32), dtype=np.uint8)
+        fpks, _ = vf.sign_batch(fseeds, np.zeros(1, np.uint8), np.zeros(nfresh + 1, np.uint32))
+        frcp = rng.integers(0, args.senders, nfresh)
+        famt = rng.integers(1, args.max_amount + 1, nfresh)
+        fmsg = np.frombuffer(b"".join(thin_transaction(pks[frcp[i]].tobytes(), int(famt[i])) for i in range(nfresh)),
+                             np.uint8)
+        _, fsig = vf.sign_batch(fseeds, fmsg, (np.arange(nfresh + 1) * 48).astype(np.uint32))
+        vf.close()
+        at = np.linspace(0, total, nfresh, endpoint=False).astype(int)
+        for i in range(nfresh - 1, -1, -1):
+            reqs.insert(int(at[i]), (wire_key(fpks[i].tobytes()), 1, wire_key(pks[frcp[i]].tobytes()), int(famt[i]),
+                                     wire_signature(fsig[i].tobytes())))
+        fresh_keys = [fpks[i].tobytes() for i in range(nfresh)]
+        total = len(reqs)
+    ready_q.put({"keys": [pks[i].tobytes() for i in range(args.senders)] + fresh_keys, "total": total, "bad": nbad,
+                 "fresh": nfresh})
     ready_q.get()  # go
     tick = 1e-3
     per_tick = max(1, int(args.rate * tick))
@@ -214,6 +236,9 @@ def main():
     ap.add_argument("--eager", type=int, default=0, help="1 = queue latency mode: also seal whenever no batch is in flight")
     ap.add_argument("--comb", type=int, default=0, help="1 = per-sender combs in each node's queue context (at2v_comb.h)")
     ap.add_argument("--senders", type=int, default=64)
+    ap.add_argument("--fresh-frac", type=float, default=0.0,
+                    help="extra transfers from first-seen senders, as a fraction of the regular traffic (one each)")
+    ap.add_argument("--cache", type=int, default=0, help="keys per node queue context with --comb (0 = 1024)")
     ap.add_argument("--bad-frac", type=float, default=0.02)
     ap.add_argument("--max-amount", type=int, default=10,
                     help="amounts in [1, max]; small enough that no sender can underflow, so the final ledger does "
@@ -225,7 +250,15 @@ def main():
     ready_q, result_q = ctx.Queue(), ctx.Queue()
     cl = ctx.Process(target=client_main, args=(inboxes, ready_q, args))
     cl.start()
-    info = ready_q.get(timeout=600)
+    info, deadline = None, time.time() + 600
+    while info is None:  # a client that dies (e.g. an exception while signing) must end the run, not stall it
+        try:
+            info = ready_q.get(timeout=5)
+        except queue_mod.Empty:
+            if not cl.is_alive():
+                raise SystemExit(f"mininode: client process exited with {cl.exitcode} before the run started")
+            if time.time() > deadline:
+                raise SystemExit("mininode: client did not get ready in 600 s")
     KEYS[:] = info["keys"]
     nodes = [ctx.Process(target=node_main_with_keys, args=(i, inboxes, result_q, args, info["keys"], info["total"]))
              for i in range(args.nodes)]
@@ -244,7 +277,7 @@ def main():
     same = len({r["ledger_sha256"] for r in res}) == 1
     out = {"metric": "AT2 mini-network ingest->verdict latency (BASELINE config 5)", "nodes": args.nodes,
            "offered_tx_per_s": args.rate, "seconds": args.seconds, "total_tx": info["total"],
-           "bad_signatures": info["bad"], "batch_B": args.batch, "delay_us": args.delay_us,
+           "bad_signatures": info["bad"], "fresh_senders": info["fresh"], "batch_B": args.batch, "delay_us": args.delay_us,
            "p50_us": max(r["lat_p50_us"] for r in res), "p99_us": max(r["lat_p99_us"] for r in res),
            "ledgers_identical": same, "all_real_applied": all(r["applied"] == info["total"] - info["bad"] for r in res), "wall_s": wall, "offered_s": offered["offered_s"], "per_node": res}
     print(json.dumps(out), flush=True)
