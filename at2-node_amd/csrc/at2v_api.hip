@@ -78,12 +78,22 @@ struct DevBuf {
 // When a launch finds the free list empty, the host learns it from the counters' asynchronous copy and compacts the
 // cache before a later launch, once no cached launch or build is in flight.
 constexpr int kClaimSlots = 8;
+struct PendingBuild {  // a launch's builds not enqueued yet (launch_shard with defer_build: after the caller's copies)
+  bool pending = false;
+  at2v::CacheArgs args{};
+  uint32_t max_claims = 0;
+  int slot = 0;
+};
 struct SenderCache {
   at2v::CacheArgs args{};
   DevBuf tags[2], entries[2];  // the live tag table / entries ([cur]) and the compaction target ([cur ^ 1])
   int cur = 0;
   DevBuf payload, free_slots, used, ctl, bcomb, claim_list[kClaimSlots];
+  // Builds run on the context's own stream (the shard's), which a caller's launches on its own streams never use: a
+  // separate build stream would share one of the process's 4 hardware queues (GPU_MAX_HW_QUEUES, round robin) with a
+  // caller's stream, whose next copy or launch then waited behind a 0.8 ms comb build (config 5 p99).
   hipStream_t build = nullptr;
+  PendingBuild deferred;
   hipEvent_t claims_ready[kClaimSlots] = {};  // launch stream, after the launch that filled slot b
   hipEvent_t slot_free[kClaimSlots] = {};     // build stream, after slot b's flip
   hipEvent_t built = nullptr;                 // build stream, after the last flip
@@ -109,6 +119,7 @@ struct Shard {
   int vgprs = 0;
   DevBuf scratch[4];
   DevBuf btab, pk, sig, msg, off, verdict;
+  hipEvent_t copied = nullptr;  // at2v_verify_batch: the verdict copy (the call waits for this, not for the builds)
   SenderCache* cache = nullptr;
 };
 
@@ -157,6 +168,7 @@ int init_shard(Shard& s, int device) {
   if (s.blocks_per_cu < 1) s.blocks_per_cu = 1;
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  AT2V_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
   if (const char* v = std::getenv("AT2V_SCRATCH_SETS")) s.sets = std::min(4, std::max(1, std::atoi(v)));
   for (int j = 0; j < s.sets; ++j) {
     AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free[j], hipEventDisableTiming));
@@ -174,7 +186,7 @@ bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) &
 
 void free_cache(SenderCache*& c) {
   if (!c) return;
-  if (c->build) (void)hipStreamSynchronize(c->build);
+  if (c->build) (void)hipStreamSynchronize(c->build);  // (the shard's stream: destroyed with the shard)
   for (DevBuf* b : {&c->tags[0], &c->tags[1], &c->entries[0], &c->entries[1], &c->payload, &c->free_slots, &c->used,
                     &c->ctl, &c->bcomb})
     b->release();
@@ -186,7 +198,6 @@ void free_cache(SenderCache*& c) {
     if (c->claims_ready[j]) (void)hipEventDestroy(c->claims_ready[j]);
     if (c->slot_free[j]) (void)hipEventDestroy(c->slot_free[j]);
   }
-  if (c->build) (void)hipStreamDestroy(c->build);
   delete c;
   c = nullptr;
 }
@@ -239,7 +250,7 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
   AT2V_TRY(hipStreamSynchronize(s.stream));
   AT2V_TRY(hipHostMalloc((void**)&c->host_ctl, c->ctl.cap, hipHostMallocDefault));
   std::memset(c->host_ctl, 0, c->ctl.cap);
-  AT2V_TRY(hipStreamCreateWithFlags(&c->build, hipStreamNonBlocking));
+  c->build = s.stream;
   AT2V_TRY(hipEventCreateWithFlags(&c->ctl_copied, hipEventDisableTiming));
   for (int j = 0; j < kClaimSlots; ++j) {  // recorded once, so the first waits are no-ops
     AT2V_TRY(hipEventCreateWithFlags(&c->claims_ready[j], hipEventDisableTiming));
@@ -276,13 +287,30 @@ hipError_t cache_before_launch(SenderCache& c, hipStream_t stream, int j) {
   return e;
 }
 
+// The builds of a cached launch's claim slot (build stream: after the launch, payloads, flip, slot free).
+hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
+  hipError_t e = hipStreamWaitEvent(c.build, c.claims_ready[b.slot], 0);
+  if (e == hipSuccess) e = at2v::launch_cache_build(b.args, b.max_claims, c.build);
+  if (e == hipSuccess) e = hipEventRecord(c.slot_free[b.slot], c.build);
+  if (e == hipSuccess) e = hipEventRecord(c.built, c.build);
+  return e;
+}
+
+// after launch_shard(.., defer_build = true) and the caller's own work on the shard stream (its verdict copy, the
+// all-gather): the deferred builds
+hipError_t flush_cache_build(Shard& s) {
+  if (!s.cache || !s.cache->deferred.pending) return hipSuccess;
+  s.cache->deferred.pending = false;
+  return enqueue_cache_build(*s.cache, s.cache->deferred);
+}
+
 // One verify launch on shard s (current device = s.device), on `stream`. The launch takes the shard's next scratch set
 // and waits for the launch that last used that set, on whatever stream that ran; launches on different streams may
 // therefore run concurrently (on one stream they are ordered anyway). Cached launches also wait for the previous cached
 // launch (the cache's tags and per-launch slot arrays are shared). The verdict words are zeroed first (fail closed).
 hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                         uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream,
-                        bool zero_verdicts = true) {
+                        bool zero_verdicts = true, bool defer_build = false) {
   const int j = (int)(s.next_set++ % (unsigned)s.sets);
   hipError_t e = hipStreamWaitEvent(stream, s.scratch_free[j], 0);
   // the cache serves the throughput kernel (launches above small_batch_max records; with combs, every launch)
@@ -306,10 +334,11 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   if (e == hipSuccess && c) {
     // claims of this launch -> payloads on the build stream (later launches use them; this one did not wait)
     e = hipEventRecord(c->claims_ready[cs], stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->build, c->claims_ready[cs], 0);
-    if (e == hipSuccess) e = at2v::launch_cache_build(ca, std::min(n, ca.capacity), c->build);
-    if (e == hipSuccess) e = hipEventRecord(c->slot_free[cs], c->build);
-    if (e == hipSuccess) e = hipEventRecord(c->built, c->build);
+    PendingBuild b{true, ca, std::min(n, ca.capacity), cs};
+    if (e == hipSuccess) {
+      if (defer_build) c->deferred = b;  // the caller enqueues it after its own work on the shard stream
+      else e = enqueue_cache_build(*c, b);
+    }
     if (e == hipSuccess) e = hipMemcpyAsync(c->host_ctl, c->ctl.p, c->ctl.cap, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipEventRecord(c->ctl_copied, stream);
     c->copy_pending = e == hipSuccess;
@@ -428,6 +457,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     for (hipEvent_t ev : s.scratch_free)
       if (ev) (void)hipEventDestroy(ev);
+    if (s.copied) (void)hipEventDestroy(s.copied);
     free_cache(s.cache);
     for (DevBuf& b : s.scratch) b.release();
     s.btab.release();
@@ -476,16 +506,20 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     if (e == hipSuccess) e = hipMemcpyAsync(s.off.p, offs.data(), (m + 1) * 4, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
       e = launch_shard(ctx, s, (const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
-                       (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (uint32_t*)s.verdict.p, s.stream);
+                       (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (uint32_t*)s.verdict.p, s.stream,
+                       true, /*defer_build=*/true);
     if (e == hipSuccess)
       e = hipMemcpyAsync(verdicts + a / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.copied, s.stream);
+    const hipError_t eb = flush_cache_build(s);  // (the next call's uploads follow the builds on this stream)
+    if (e == hipSuccess) e = eb;
     if (e != hipSuccess) rc = hip_code(e);
   }
-  // shards run concurrently on their own devices/streams; wait for all of them
+  // shards run concurrently on their own devices/streams; wait for all of them (not for the builds behind them)
   for (size_t g = 0; g < G; ++g) {
     Shard& s = ctx->shards[g];
     if (hipSetDevice(s.device) != hipSuccess) continue;
-    hipError_t e = hipStreamSynchronize(s.stream);
+    hipError_t e = hipEventSynchronize(s.copied);
     if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
   (void)hipSetDevice(prev);
@@ -628,7 +662,7 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
   if (e == hipSuccess && m)
     e = launch_shard(ctx, s, (const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
                      (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (uint32_t*)s.verdict.p, s.stream,
-                     /*zero_verdicts=*/false);
+                     /*zero_verdicts=*/false, /*defer_build=*/true);
   int rc = hip_code(e);
   // The all-gather runs in rounds of at most kGatherWindow words per rank through buffers allocated at
   // at2v_comm_init_rank, so no allocation stands between a rank and the collectives: every rank issues the same
@@ -664,6 +698,7 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
   if (rc == AT2V_OK && ra != ncclSuccess) rc = AT2V_E_RCCL;
   if (rc == AT2V_OK && es != hipSuccess) rc = hip_code(es);
   if (rc == AT2V_OK && got) rc = AT2V_E_PEER;
+  (void)flush_cache_build(s);  // after the collectives (a failed enqueue only leaves keys unbuilt)
   (void)hipSetDevice(prev);
   return rc;
 }

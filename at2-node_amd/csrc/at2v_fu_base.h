@@ -58,6 +58,12 @@ __device__ AT2V_INLINE uint32_t at2v_udbl32(uint32_t x) {
 #ifndef AT2V_FU_ASM
 #define AT2V_FU_ASM 1
 #endif
+// AT2V_FU_FUSED = 1: every single product is ONE asm statement (accumulator in the clobbered pair v[254:255], limbs and
+// carries extracted inside the string), so hipcc's one-state pad after each inline asm (an s_nop 0 before the carry
+// shift) comes once per product instead of once per column (tools/gen_fu.py emit_fused)
+#ifndef AT2V_FU_FUSED
+#define AT2V_FU_FUSED 0
+#endif
 #else
 #define AT2V_UX2(x) AT2V_USC(2u, (x))
 #undef AT2V_FU_ASM

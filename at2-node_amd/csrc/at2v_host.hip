@@ -32,7 +32,9 @@ constexpr size_t kSingleCopyMax = 2u << 20;
 struct HipBackend {
   at2v_ctx* ctx = nullptr;
   int device = 0;
-  hipStream_t h2d = nullptr, comp[2] = {nullptr, nullptr}, d2h = nullptr;
+  // three streams of the queue + the context's own (which runs the sender-cache builds): four, one hardware queue each
+  // (GPU_MAX_HW_QUEUES = 4), so no verify or copy of the latency path waits behind a comb build in a shared queue
+  hipStream_t h2d = nullptr, comp[2] = {nullptr, nullptr};
   unsigned launches = 0;
 
   int init(const at2v_queue_opts& o) {
@@ -48,12 +50,11 @@ struct HipBackend {
     if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     for (hipStream_t& c : comp)
       if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
-    if (hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     return AT2V_OK;
   }
   void fini() {
     if (hipSetDevice(device) == hipSuccess) {
-      for (hipStream_t* s : {&h2d, &comp[0], &comp[1], &d2h})
+      for (hipStream_t* s : {&h2d, &comp[0], &comp[1]})
         if (*s) {
           (void)hipStreamSynchronize(*s);
           (void)hipStreamDestroy(*s);
@@ -106,7 +107,7 @@ struct HipBackend {
     delete d;
     s.backend = nullptr;
   }
-  // H2D on h2d -> verify on comp[k % 2] (waits for its upload) -> D2H on d2h (waits for its kernel)
+  // H2D on h2d -> verify on comp[k % 2] (waits for its upload) -> D2H on the same comp stream
   int launch(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
     hipStream_t comp = this->comp[launches++ & 1];
@@ -126,10 +127,8 @@ struct HipBackend {
     const int rc = at2v_verify_batch_device(ctx, (const uint8_t*)d->pk, (const uint8_t*)d->sig, (const uint8_t*)d->msg,
                                             s.msg_used, (const uint32_t*)d->off, n, (uint32_t*)d->ver, comp);
     if (rc) return rc;
-    e = hipEventRecord(d->verified, comp);
-    if (e == hipSuccess) e = hipStreamWaitEvent(d2h, d->verified, 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.verdicts, d->ver, words * 4, hipMemcpyDeviceToHost, d2h);
-    if (e == hipSuccess) e = hipEventRecord(d->done, d2h);
+    e = hipMemcpyAsync(s.verdicts, d->ver, words * 4, hipMemcpyDeviceToHost, comp);
+    if (e == hipSuccess) e = hipEventRecord(d->done, comp);
     return e == hipSuccess ? AT2V_OK : AT2V_E_HIP;
   }
   int wait(at2v::QueueSlot& s) {

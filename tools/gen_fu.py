@@ -284,6 +284,9 @@ def emit_fn(name, colsets, is_mul, cheap_wrap):
             else:
                 out.append(f"  const uint32_t {nm(q, src, i, s)} = AT2V_USC({s}u, {src}{q}_{i});")
     out.append("  " + " ".join(f"uint64_t c{q} = 0;" for q in ps))
+    if nway == 1:
+        out += emit_fused(colsets[0], gsrc, nm)
+        out.append("#else")
     for k in range(10):
         cs = [cols[k] for cols in colsets]
         assert all(len(c) == len(cs[0]) for c in cs)
@@ -334,6 +337,8 @@ def emit_fn(name, colsets, is_mul, cheap_wrap):
                 expr = f"AT2V_UMAD({nm(q, 'f', i, a)}, {nm(q, gsrc, j, b)}, {expr})"
             out.append(f"  {{ const uint64_t hk = {expr}; c{q} = hk >> {W[k]}; h{q}.v[{k}] = (uint32_t)hk & 0x{(1 << W[k]) - 1:x}u; }}")
         out.append("#endif")
+    if nway == 1:
+        out.append("#endif  // AT2V_FU_FUSED")
     # wrap: t = r0 + 19 c9
     for q, cw in zip(ps, cheap_wrap):
         out.append("  {")
@@ -346,6 +351,44 @@ def emit_fn(name, colsets, is_mul, cheap_wrap):
         out.append("  }")
     out.append("}")
     return "\n".join(out)
+
+
+def emit_fused(cols, gsrc, nm):
+    """AT2V_FU_FUSED: the whole product as ONE asm statement. The column accumulator lives in the clobbered pair
+    v[254:255]: column k's MAD chain ends there, v_and_b32 takes limb k out of its low half (into an output operand) and
+    v_lshrrev_b64 shifts the pair in place into the carry that starts column k+1's chain; column 9's carry goes to an
+    output operand for the wrap. hipcc pads one wait state after every inline asm whose output a VALU reads next (it
+    cannot see inside the string); per column that was one s_nop per product column, here it is one per product. No
+    VALU->VALU pair inside the string needs a wait state on gfx950 (no DPP, SDWA, trans or readlane consumers)."""
+    out = ["#if AT2V_FU_ASM && AT2V_FU_FUSED", "  {"]
+    ins, idx = [], {}
+
+    def reg(e):
+        if e not in idx:
+            idx[e] = len(ins)
+            ins.append(e)
+        return idx[e]
+    lines = []
+    nout = 11  # r0..r9, c9
+    for k in range(10):
+        for t, (i, a, j, b) in enumerate(cols[k]):
+            ra, rb = reg(nm("", "f", i, a)), reg(nm("", gsrc, j, b))
+            addend = ("0" if k == 0 else "v[254:255]") if t == 0 else "v[254:255]"
+            lines.append(f"v_mad_u64_u32 v[254:255], vcc, %{ra + nout}, %{rb + nout}, {addend}")
+        lines.append(f"v_and_b32 %{k}, 0x{(1 << W[k]) - 1:x}, v254")
+        if k < 9:
+            lines.append(f"v_lshrrev_b64 v[254:255], {W[k]}, v[254:255]")
+        else:
+            lines.append(f"v_lshrrev_b64 %10, {W[k]}, v[254:255]")
+    out.append("    uint32_t r0, r1, r2, r3, r4, r5, r6, r7, r8, r9;")
+    out.append('    asm("' + "\\n\\t".join(lines) + '"')
+    out.append('        : ' + ", ".join(f'"=&v"(r{k})' for k in range(10)) + ', "=&v"(c)')
+    out.append('        : ' + ", ".join(f'"v"({e})' for e in ins))
+    out.append('        : "vcc", "v254", "v255");')
+    out.append("    h.v[0] = r0; h.v[1] = r1; h.v[2] = r2; h.v[3] = r3; h.v[4] = r4;")
+    out.append("    h.v[5] = r5; h.v[6] = r6; h.v[7] = r7; h.v[8] = r8; h.v[9] = r9;")
+    out.append("  }")
+    return out
 
 
 def lit(limbs):

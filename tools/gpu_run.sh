@@ -6,6 +6,8 @@
 #   suite         pytest -m gpu (the whole parity / boundary / cache suite)
 #   tests=<expr>  pytest -m gpu -k <expr>
 #   files=<a,b>   pytest -m gpu on those test files
+#   probe=<expr>  pytest -m gpu -k <expr>, output gpu_probe<N>.txt; test failures (exit 1) do not end the run, any other
+#                 failure (time limit, crash) does
 #   smoke         __graft_entry__.smoke()
 #   bench         python bench.py (the default driver line: config 2 + at2_traffic + roofline + cpu_baseline)
 #   bench1        python bench.py with the PMC passes and CPU baseline off (a quick rate check)
@@ -27,6 +29,7 @@ run() {  # run <name> <seconds> <cmd...>: stdout+stderr to $D/<name>.txt, tail o
   timeout -k 10 "$t" "$@" > "$D/$name.txt" 2>&1 || { echo "[gpu_run] $name FAILED rc=$?"; tail -40 "$D/$name.txt"; exit 1; }
   tail -3 "$D/$name.txt"
 }
+NPROBE=0
 for st in "$@"; do
   case "$st" in
     suite) run gpu_tests 1100 python -u -m pytest tests -m gpu -v --maxfail=3 --timeout 300 --timeout-method thread
@@ -36,6 +39,14 @@ for st in "$@"; do
              cp gpurun_out/config5_*.json $D/ 2>/dev/null ;;
     tests=*) run gpu_tests_k 900 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread -k "${st#tests=}"
              cp gpurun_out/config5_*.json $D/ 2>/dev/null ;;
+    probe=*) NPROBE=$((NPROBE + 1))
+             echo "[gpu_run] probe$NPROBE: ${st#probe=}"
+             timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+               -k "${st#probe=}" > $D/gpu_probe$NPROBE.txt 2>&1
+             rc=$?
+             tail -3 $D/gpu_probe$NPROBE.txt
+             mkdir -p $D/probe$NPROBE && cp gpurun_out/config5_*.json $D/probe$NPROBE/ 2>/dev/null
+             [ $rc -le 1 ] || { echo "[gpu_run] probe$NPROBE FAILED rc=$rc"; exit 1; } ;;
     smoke) run smoke 180 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 500 python3 bench.py
            grep '^{' $D/bench.txt > $D/bench.json ;;

@@ -66,10 +66,24 @@ def main():
         first_us = None
         if a.comb:
             vc = at2v.BatchVerifier(device=0, sender_cache=1024, sender_comb=True)
-            # a running node's context: one earlier launch (other keys) before the measured one, so the measurement is
-            # the first payload of new senders, not the first launch of a new context (that costs ~0.7 ms more, once)
-            wp, wg, wm, wf = o.gen_records(0x4154325F, 1 << 30, 64, a.msg_len)
-            assert vc.verify_batch(wp, wg, wm, wf).all()
+            # a running node's context: earlier launches (other keys, on the measured stream, both scratch sets) before
+            # the measured one, so the measurement is the first payload of new senders, not the first use of a new
+            # context (its first launch per scratch set costs ~0.7 ms more, once: `first_launch_fresh_context_us`)
+            wp, wg, wm, wf = o.gen_records(0x4154325F, 1 << 30, 128, a.msg_len)
+            wd = [torch.from_numpy(x.reshape(-1).copy()).cuda() for x in (wp, wg)]
+            wdm = torch.from_numpy(np.concatenate([wm, np.zeros(16, np.uint8)])).cuda()
+            wv = torch.zeros(2, dtype=torch.int32, device="cuda")
+            fresh_ctx = []
+            for h in range(2):
+                wo = torch.from_numpy((wf[64 * h:64 * h + 65] - wf[64 * h]).view(np.int32).copy()).cuda()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                vc.verify_batch_device(wd[0].data_ptr() + 64 * h * 32, wd[1].data_ptr() + 64 * h * 64,
+                                       wdm.data_ptr() + int(wf[64 * h]), int(wf[64 * h + 64] - wf[64 * h]),
+                                       wo.data_ptr(), 64, wv.data_ptr(), s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                fresh_ctx.append(e0.elapsed_time(e1) * 1e3)
             vc.info()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -131,6 +145,7 @@ def main():
         if first_us is not None:
             out["sizes"][B]["first_launch_new_keys_us"] = first_us
             out["sizes"][B]["first_combs_ready_us"] = combs_ready_us
+            out["sizes"][B]["first_launch_fresh_context_us"] = fresh_ctx
         print(B, json.dumps(out["sizes"][B]), file=sys.stderr)
     q.close()
     v.close()
