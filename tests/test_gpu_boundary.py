@@ -176,6 +176,7 @@ def test_config5_mininode_4_nodes(at2v_mod):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.clean_gpu
 def test_config5_mininode_eager_latency(at2v_mod):
     """BASELINE config 5 in the queue's latency mode (seal whenever no batch is in flight) with the low-latency
     kernel: same correctness bar as above, plus a latency gate: every node's queue
@@ -196,6 +197,7 @@ def test_config5_mininode_eager_latency(at2v_mod):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.clean_gpu
 def test_config5_mininode_comb_latency(at2v_mod):
     """BASELINE config 5 in latency mode with per-sender combs in every node's queue (AT2V_QUEUE_SENDER_COMB): the 64
     client keys get combs on first sight, then every small batch verifies by table additions (at2v_comb.h). Same
@@ -216,12 +218,14 @@ def test_config5_mininode_comb_latency(at2v_mod):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.clean_gpu
 def test_config5_mininode_fresh_senders_latency(at2v_mod):
     """VERDICT r3 "Next" 4: config 5 with combs and a stream of first-seen senders (2% of the traffic comes from keys
-    no node has seen, each sending once). A batch holding a fresh key verifies its chunk by the two-wave half-size
-    four-wave split half-size check in the same kernel instead of waiting for a comb build, and the comb is built on the
-    context's stream after the launch's copy-out, for later payloads. Same correctness bar; latency gates on every node's queue: p50 <= 0.4 ms and p99 <= 1.0 ms (round 3's
-    first-seen launch alone was 0.82-0.94 ms of device time). Results in gpurun_out/config5_fresh.json."""
+    no node has seen, each sending once). A batch holding a fresh key verifies its chunk by the four-wave split
+    half-size check in the same kernel instead of waiting for a comb build, and the comb is built on the context's
+    stream after the launch's copy-out, for later payloads. Same correctness bar; latency gates on every node's queue:
+    p50 <= 0.4 ms and p99 <= 1.0 ms (round 3's first-seen launch alone was 0.82-0.94 ms of device time). Results in
+    gpurun_out/config5_fresh.json."""
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mininode.py"), "--nodes", "4", "--rate", "20000",
                           "--seconds", "2", "--batch", "1024", "--delay-us", "1000", "--eager", "1", "--comb", "1",

@@ -68,7 +68,7 @@ def main():
             vc = at2v.BatchVerifier(device=0, sender_cache=1024, sender_comb=True)
             # a running node's context: earlier launches (other keys, on the measured stream, both scratch sets) before
             # the measured one, so the measurement is the first payload of new senders, not the first use of a new
-            # context (its first launch per scratch set costs ~0.7 ms more, once: `first_launch_fresh_context_us`)
+            # context (`first_launch_fresh_context_us`: these two launches, each after an idle pause)
             wp, wg, wm, wf = o.gen_records(0x4154325F, 1 << 30, 128, a.msg_len)
             wd = [torch.from_numpy(x.reshape(-1).copy()).cuda() for x in (wp, wg)]
             wdm = torch.from_numpy(np.concatenate([wm, np.zeros(16, np.uint8)])).cuda()
@@ -86,6 +86,13 @@ def main():
                 fresh_ctx.append(e0.elapsed_time(e1) * 1e3)
             vc.info()
             torch.cuda.synchronize()
+            # a node's GPU is busy between payloads; after the host-side pauses above an idle GPU has dropped its clock,
+            # and a launch right then runs ~2.5x slower (first_launch_fresh_context_us). ~10 ms of other work on the
+            # same stream first, then the launch.
+            busy = torch.randn(4096, 4096, device="cuda")
+            for _ in range(8):
+                busy = busy @ busy
+                busy /= busy.abs().max()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t_first = time.perf_counter()
             e0.record(s)
