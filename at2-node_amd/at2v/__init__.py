@@ -206,7 +206,7 @@ class BatchVerifier:
         """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
         0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel.
         sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off).
-        sender_comb: with sender_cache, also keep a comb of -A per cached key (2.1 MB of HBM each, plus one 67 MB comb
+        sender_comb: with sender_cache, also keep a comb of -A per cached key (1.7 MB of HBM each, plus one 67 MB comb
         of B per context; include/at2v.h): chunks whose senders are all cached verify by table additions only
         (at2v_comb.h), launches of every size."""
         self._lib = load_library()

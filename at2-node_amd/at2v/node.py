@@ -145,7 +145,7 @@ class IngestQueue:
                  max_msg_bytes: int = 256, depth: int = 3, eager: bool = False, sender_comb: bool = False,
                  sender_cache: int = 0):
         """eager: also seal whenever no batch is in flight (latency mode); sender_comb: per-sender combs in the queue's
-        context (at2v_comb.h) for `sender_cache` keys (0 = 1024; 2.1 MB of HBM per key)"""
+        context (at2v_comb.h) for `sender_cache` keys (0 = 1024; 1.7 MB of HBM per key)"""
         from . import _POLICIES
         self._lib = _lib()
         o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth,

@@ -2,7 +2,8 @@
 //
 // AT2 senders issue consecutive sequences (/root/reference/src/bin/server/accounts/account.rs:36-43): one public key A
 // signs many payloads. For such a key the device keeps a comb of -A, C[i][j] = [j 2^(10i)](-A) for i = 0..25, j = 0..512
-// (cached form), next to the context's comb of B, D[i][j] = [j 2^(16i)]B for i = 0..15, j = 0..2^15 (affine Niels).
+// (affine Niels, or cached form with AT2V_COMB_NIELS=0), next to the context's comb of B, D[i][j] = [j 2^(16i)]B for
+// i = 0..15, j = 0..2^15 (affine Niels).
 // Then dalek's point R' = [k](-A) + [s]B is a sum of 26 + 16 table entries, no doublings:
 //   k = sum_i e_i 2^(10i), e_i in [-512, 511] (sc_recode_w) ->  [k](-A) = sum_i +-C[i][|e_i|]
 //   s = sum_i f_i 2^(16i), f_i in [-2^15, 2^15) (sc_recode16) ->  [s]B   = sum_i +-D[i][|f_i|]
@@ -11,11 +12,10 @@
 // those of the ladder kernels (and of the oracle), for every key the comb was built from, small-order and mixed-order
 // keys included; a key that fails dalek's decode has verdict 0 whatever the comb holds.
 //
-// Cost per verify: 26 additions with cached entries (8 M) + 16 mixed additions (7 M) + one inversion (254 S + 11 M; shared
-// by two records in the throughput kernel) + SHA-512, against the half-size ladder's 2 exponentiations + 2 tables + 33
-// windows: ~4x fewer multiplications. The comb of one key is 26 x 513 x 160 B = 2.1 MB (10-bit windows),
-// built once (comb_build_lane).
-//   TabC  : prefetch(stage, i, j) / load_prefetched(stage, gu_cached&)   entry C[i][j] of this lane's key
+// Cost per verify: 42 mixed additions (7 M) + one inversion (254 S + 11 M; shared by four records in the throughput
+// kernel) + SHA-512, against the half-size ladder's 2 exponentiations + 2 tables + 33 windows: ~5x fewer
+// multiplications. The comb of one key is 26 x 513 x 128 B = 1.7 MB (10-bit windows), built once (comb_build_lane).
+//   TabC  : prefetch(stage, i, j) / load_prefetched(stage, CombEntry&)   entry C[i][j] of this lane's key
 //   TabBC : prefetch(stage, i, j) / load_prefetched(stage, gu_niels&)    entry D[i][j]
 // Two stages alternate: the entry of the next addition is fetched while this one is computed. The low-latency kernel
 // splits one record's work over four waves (decode R | 16 B entries | SHA-512 + 13 A entries | SHA-512 + 13 A entries)
@@ -26,7 +26,7 @@
 
 namespace at2v {
 
-// A comb window: signed radix-2^w digits of k (w = AT2V_COMB_BITS). w = 10 (default): 26 positions x 513 entries, 2.1 MB
+// A comb window: signed radix-2^w digits of k (w = AT2V_COMB_BITS). w = 10 (default): 26 positions x 513 entries, 1.7 MB
 // per key; w = 8: 32 positions x 129 entries, 660 KB per key, 6 additions more per verify (368.4 vs 399.9 M/s on 64-sender
 // traffic, profiles/r03z).
 #ifndef AT2V_COMB_BITS
@@ -47,7 +47,18 @@ constexpr int kCombWideMaxKeys = 256;  // new keys per launch up to which the wi
 constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
 constexpr int kBCombPos = 16;         // B comb positions (radix 2^16)
 constexpr int kBCombEntries = 32769;  // j = 0..2^15
-constexpr int kCombGranules = 10;     // cached point: 40 words
+// A-comb entry form. 1 (default since round 4): affine Niels (y+x, y-x, 2dxy), 30 words in 8 granules = one 128-byte
+// line, mixed additions (7 M); the builder normalises its lane's entries with one inversion (Montgomery's trick).
+// 0: cached (Y+X, Y-X, 2Z, 2dT), 40 words in 10 granules (two or three lines), 8 M additions.
+#ifndef AT2V_COMB_NIELS
+#define AT2V_COMB_NIELS 1
+#endif
+constexpr bool kCombNiels = AT2V_COMB_NIELS != 0;
+template <bool kNiels> struct CombEntrySel { using type = gu_cached; };
+template <> struct CombEntrySel<true> { using type = gu_niels; };
+using CombEntry = CombEntrySel<kCombNiels>::type;
+constexpr int kCombGranules = kCombNiels ? 8 : 10;
+constexpr int kCombWords = kCombGranules * 4;
 constexpr size_t kCombBytes = (size_t)kCombPos * kCombEntries * kCombGranules * 16;  // per key
 
 // R' (p2) encoded as dalek's CompressedEdwardsY (y canonical, sign bit = low bit of canonical x) == R_bytes
@@ -123,7 +134,7 @@ AT2V_HD AT2V_INLINE int comb_bdigit(const uint32_t sd[8], int i) {
   return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000;
 }
 
-// acc += sum over positions i in [i0, i1) of the signed entry C[i][e_i] (A comb, cached form, kAComb) or D[i][f_i] (B
+// acc += sum over positions i in [i0, i1) of the signed entry C[i][e_i] (A comb, kAComb: CombEntry) or D[i][f_i] (B
 // comb, affine Niels). The entry of addition m + 1 is fetched (into the other stage) while m is computed.
 template <bool kAComb, class Tab>
 AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int i1, const Tab& tab) {
@@ -141,7 +152,7 @@ AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int
       const int m = i + h;
       if (m >= i1) break;  // an odd count (wave-uniform)
       const int en = m + 1 < i1 ? digit(m + 1) : 0;
-      if constexpr (kAComb) {
+      if constexpr (kAComb && !kCombNiels) {
         gu_cached ca;
         tab.load_prefetched(h, ca);
         if (m + 1 < i1) tab.prefetch(h ^ 1, m + 1, en < 0 ? -en : en);
@@ -225,15 +236,31 @@ AT2V_HD AT2V_INLINE int comb_check_split(const gu_p3& R, const gu_p3& Pa0, const
 }
 
 // One lane's share of the comb of key A, with 2^kPartsLog2 lanes per position: position pos (0..kCombPos-1), part h ->
-// entries j = kPart h + 1 .. kPart (h + 1) (kPart = 2^(w-1-kPartsLog2)) of C[pos][j] = [j 2^(w pos)](-A), cached form,
-// through store(j, const gu_cached&); the h = 0 lane also stores j = 0 (the identity). kCombPos 2^kPartsLog2 lanes
-// (pos = lane >> kPartsLog2, h = the low bits) build the whole comb; a lane with pos >= kCombPos stores nothing.
-// Every lane decodes A (dalek rules) and returns the decode verdict; an undecodable A yields a comb that no verdict
-// depends on. Per lane: (kCombPos - 1) w doublings (the position chain), log2(kPart) doublings and h additions to
-// the part's first multiple, kPart additions (w = 10: 8 parts, 256 doublings and at most 71 additions; 2 parts, 258
-// doublings and at most 257 additions).
-template <int kPartsLog2, class Store>
-AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, Store&& store) {
+// entries j = kPart h + 1 .. kPart (h + 1) (kPart = 2^(w-1-kPartsLog2)) of C[pos][j] = [j 2^(w pos)](-A), written through
+// mem.put(j, words) (kCombWords words in CombEntry's layout); the h = 0 lane also writes j = 0 (the identity). kCombPos
+// 2^kPartsLog2 lanes (pos = lane >> kPartsLog2, h = the low bits) build the whole comb; a lane with pos >= kCombPos
+// writes nothing. Every lane decodes A (dalek rules) and returns the decode verdict; an undecodable A yields a comb that
+// no verdict depends on. Per lane: (kCombPos - 1) w doublings (the position chain), log2(kPart) doublings and h
+// additions to the part's first multiple, kPart additions (w = 10: 8 parts, 256 doublings and at most 71 additions; 2
+// parts, 258 doublings and at most 257 additions). Affine entries (kCombNiels) take two passes over the lane's own
+// entries: pass 1 writes (X pi', Y pi', Z) with pi' the product of the earlier Z's, one inversion of the product of all
+// of them, pass 2 (backwards, mem.get) turns each into (y+x, y-x, 2dxy) with x = X pi' / pi: 8 M more per entry.
+template <class Mem>
+AT2V_HD AT2V_INLINE void comb_put_fu3(Mem& mem, int j, const fu& a, const fu& b, const fu& c) {
+  uint32_t w[kCombWords];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) {
+    w[q] = a.v[q];
+    w[10 + q] = b.v[q];
+    w[20 + q] = c.v[q];
+  }
+#pragma unroll
+  for (int q = 30; q < kCombWords; ++q) w[q] = 0;
+  mem.put(j, w);
+}
+
+template <int kPartsLog2, class Mem>
+AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, Mem& mem) {
   constexpr int kPartBits = kCombBits - 1 - kPartsLog2;
   constexpr int kPart = 1 << kPartBits;
   gu_p3 P;
@@ -282,19 +309,73 @@ AT2V_HD AT2V_INLINE int comb_build_lane(const uint32_t Aw[8], int pos, int h, St
       gu_p1p1_to_p3(S, t);
     }
   }
-  if (h == 0) {
-    gu_cached id;
-    gu_cached_identity(id);
-    store(0, id);
-  }
-  gu_cached cj;
+  const int j0 = kPart * h + 1;
+  if constexpr (!kCombNiels) {
+    if (h == 0) {
+      gu_cached id;
+      gu_cached_identity(id);
+      mem.put(0, reinterpret_cast<const uint32_t*>(&id));
+    }
+    gu_cached cj;
 #pragma unroll 1
-  for (int m = 0; m < kPart; ++m) {
-    gu_p3_to_cached(cj, S);
-    store(kPart * h + 1 + m, cj);
-    if (m + 1 < kPart) {
-      gu_add(t, S, c1);
-      gu_p1p1_to_p3(S, t);
+    for (int m = 0; m < kPart; ++m) {
+      gu_p3_to_cached(cj, S);
+      mem.put(j0 + m, reinterpret_cast<const uint32_t*>(&cj));
+      if (m + 1 < kPart) {
+        gu_add(t, S, c1);
+        gu_p1p1_to_p3(S, t);
+      }
+    }
+  } else {
+    if (h == 0) {
+      fu one, zero;
+      fu_1(one);
+      fu_0(zero);
+      comb_put_fu3(mem, 0, one, one, zero);  // identity: y+x = 1, y-x = 1, 2dxy = 0
+    }
+    fu pi;  // pass 1: pi = Z_0 ... Z_m; entry m holds (X_m pi_(m-1), Y_m pi_(m-1), Z_m)
+#pragma unroll 1
+    for (int m = 0; m < kPart; ++m) {
+      if (m == 0) {
+        comb_put_fu3(mem, j0, S.X, S.Y, S.Z);
+        pi = S.Z;
+      } else {
+        fu xp, yp;
+        fu_mulc(xp, S.X, pi);
+        fu_mulc(yp, S.Y, pi);
+        comb_put_fu3(mem, j0 + m, xp, yp, S.Z);
+        fu_mulc(pi, pi, S.Z);
+      }
+      if (m + 1 < kPart) {
+        gu_add(t, S, c1);
+        gu_p1p1_to_p3(S, t);
+      }
+    }
+    fu inv;  // 1 / pi_m, m from the last entry down
+    fu_invert(inv, pi);
+#pragma unroll 1
+    for (int m = kPart - 1; m >= 0; --m) {
+      uint32_t w[kCombWords];
+      mem.get(j0 + m, w);
+      fu xp, yp, z, x, y;
+#pragma unroll
+      for (int q = 0; q < 10; ++q) {
+        xp.v[q] = w[q];
+        yp.v[q] = w[10 + q];
+        z.v[q] = w[20 + q];
+      }
+      fu_mulc(x, xp, inv);
+      fu_mulc(y, yp, inv);
+      fu_mulc(inv, inv, z);
+      gu_niels n;
+      fu_add(n.ypx, y, x);
+      fu_carry(n.ypx);
+      fu_sub(n.ymx, y, x, FU_KC);
+      fu_carry(n.ymx);
+      fu xy;
+      fu_mulc(xy, x, y);
+      fu_mulc(n.xy2d, xy, FU_D2);
+      comb_put_fu3(mem, j0 + m, n.ypx, n.ymx, n.xy2d);
     }
   }
   return ok;

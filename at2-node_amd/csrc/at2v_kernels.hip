@@ -239,7 +239,7 @@ struct DevTabB {
 };
 
 // Comb entries (at2v_comb.h) by LDS-DMA into two alternating per-wave stages: the entry of the next addition lands while
-// this one is computed. TabC: C[i][j] of this lane's key (cached form, 10 granules); TabBC: D[i][j] (affine Niels, 8).
+// this one is computed. TabC: C[i][j] of this lane's key (CombEntry, kCombGranules); TabBC: D[i][j] (affine Niels, 8).
 struct DevComb {
   const int4* base;  // this lane's key's comb
   int4* stage[2];    // this wave's two 10 KiB stages (wave-uniform)
@@ -252,19 +252,21 @@ struct DevComb {
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
                                        (__attribute__((address_space(3))) void*)(stage[st] + q * 64), 16, 0, 0);
   }
-  template <class Cached>
-  __device__ AT2V_INLINE void load_prefetched(int st, Cached& c) const {
-    static_assert(sizeof(Cached) == 160, "cached point: 40 words");
+  __device__ AT2V_INLINE void load_prefetched(int st, CombEntry& c) const {
+    static_assert(sizeof(CombEntry) <= (size_t)kCombWords * 4, "comb entry words");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int32_t* w = reinterpret_cast<int32_t*>(&c);
+    int32_t w[kCombWords];
 #pragma unroll
-    for (int q = 0; q < 10; ++q) {
+    for (int q = 0; q < kCombGranules; ++q) {
       const int4 v = stage[st][q * 64 + lane];
       w[4 * q] = v.x;
       w[4 * q + 1] = v.y;
       w[4 * q + 2] = v.z;
       w[4 * q + 3] = v.w;
     }
+    int32_t* cw = reinterpret_cast<int32_t*>(&c);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(CombEntry) / 4); ++q) cw[q] = w[q];
   }
 };
 struct DevBComb {
@@ -1625,12 +1627,27 @@ __device__ AT2V_INLINE void comb_claim(const CacheArgs& c, uint32_t t, int g) {
   entry_key(a, ent);
   int4* cb = c.payload + (size_t)e.y * (kCombBytes / 16);
   const int pos = g >> kPartsLog2;
-  const int ok = comb_build_lane<kPartsLog2>(a, pos, g & ((1 << kPartsLog2) - 1), [&](int j, const gu_cached& p) {
-    const int32_t* w = reinterpret_cast<const int32_t*>(&p);
-    int4* dst = cb + ((size_t)pos * kCombEntries + j) * kCombGranules;
+  struct Mem {  // this position's entries in payload u (a lane reads back only entries it wrote itself)
+    int4* row;
+    __device__ AT2V_INLINE void put(int j, const uint32_t* w) const {
+      int4* dst = row + (size_t)j * kCombGranules;
 #pragma unroll
-    for (int q = 0; q < kCombGranules; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-  });
+      for (int q = 0; q < kCombGranules; ++q)
+        dst[q] = make_int4((int)w[4 * q], (int)w[4 * q + 1], (int)w[4 * q + 2], (int)w[4 * q + 3]);
+    }
+    __device__ AT2V_INLINE void get(int j, uint32_t* w) const {
+      const int4* src = row + (size_t)j * kCombGranules;
+#pragma unroll
+      for (int q = 0; q < kCombGranules; ++q) {
+        const int4 v = src[q];
+        w[4 * q] = (uint32_t)v.x;
+        w[4 * q + 1] = (uint32_t)v.y;
+        w[4 * q + 2] = (uint32_t)v.z;
+        w[4 * q + 3] = (uint32_t)v.w;
+      }
+    }
+  } mem{cb + (size_t)(pos < kCombPos ? pos : 0) * kCombEntries * kCombGranules};
+  const int ok = comb_build_lane<kPartsLog2>(a, pos, g & ((1 << kPartsLog2) - 1), mem);
   if (g == 0) reinterpret_cast<int*>(ent + 2)[0] = ok;
 }
 

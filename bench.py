@@ -38,10 +38,10 @@ MAC_PER_VERIFY = 100 * FIELD_MUL_PER_VERIFY + 55 * FIELD_SQ_PER_VERIFY  # 175,71
 # VALU rate on gfx950 (profiles/r01_ubench_valu.txt): one wave64 instruction per 4 cycles per SIMD
 # = 16 lane-MACs/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz.
 MAC_PEAK = 256 * 4 * 16 * 2.4e9  # 3.93e13 MAC/s
-# The comb path of AT2 traffic (DESIGN.md §10d, 10-bit A windows, four records per lane): 26 cached-point additions
-# (8 M) + 16 mixed additions (7 M), a quarter of a shared inversion (254 S + 11 M) + 2.25 M of Montgomery's trick over
-# four Z's, and 2 M to encode R': 327 M + 63.5 S per verify.
-COMB_MAC_PER_VERIFY = 100 * 327 + 55 * 63.5  # 36,192.5
+# The comb path of AT2 traffic (DESIGN.md §10d, 10-bit A windows, four records per lane): 26 + 16 mixed additions with
+# affine entries (7 M), a quarter of a shared inversion (254 S + 11 M) + 2.25 M of Montgomery's trick over four Z's,
+# and 2 M to encode R': 301 M + 63.5 S per verify.
+COMB_MAC_PER_VERIFY = 100 * 301 + 55 * 63.5  # 33,592.5
 HBM_PEAK_GBS = 8000.0
 
 
@@ -429,8 +429,8 @@ def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
                          "achieved": n * steps / dt * COMB_MAC_PER_VERIFY / 1e12, "peak": MAC_PEAK / 1e12,
                          "unit": "Tops/s (32x32->64 integer MAC, v_mad_u64_u32)",
                          "frac": n * steps / dt * COMB_MAC_PER_VERIFY / MAC_PEAK,
-                         "note": "at the wall-clock step rate (launch gaps included); 327 M + 63.5 S per verify "
-                                 "(four records per lane share one inversion)"},
+                         "note": "at the wall-clock step rate (launch gaps included); 301 M + 63.5 S per verify "
+                                 "(affine comb entries; four records per lane share one inversion)"},
             "method": f"{n} records per step (100-byte M) signed by {senders} repeating senders (GPU generator, record i "
                       f"by sender i % {senders}), sender_cache 1024 + sender_comb: chunks whose senders are all cached "
                       "verify by comb additions (DESIGN §10d); combs built in the warm-up. kernel_ms = device time per "

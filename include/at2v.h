@@ -55,8 +55,8 @@ typedef struct {
                                first time is verified without the cache; its entry is built on the context's build
                                stream after that launch and serves later launches. When the capacity is reached, the
                                least recently used entries (by launch) are replaced; up to 3/4 of the capacity stays. */
-  uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(10i)](-A), 2.1 MB
-                               per key, sender_cache x 2.1 MB per device, plus a 67 MB comb of B per context), and a
+  uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(10i)](-A), 1.7 MB
+                               per key, sender_cache x 1.7 MB per device, plus a 67 MB comb of B per context), and a
                                64-record chunk whose senders are all cached is verified by 42 table additions and one
                                inversion instead of the doubling ladder (~3x fewer multiplications; launches of any size,
                                small batches included). Same verdicts. 0 = off. */
@@ -216,7 +216,7 @@ typedef struct {
   uint32_t flags;         /* AT2V_QUEUE_EAGER: also seal whenever no batch is in flight; AT2V_QUEUE_SENDER_COMB:
                              per-sender combs (at2v_opts.sender_comb) */
   uint32_t sender_cache;  /* with AT2V_QUEUE_SENDER_COMB: keys the queue's context caches (at2v_opts.sender_cache,
-                             2.1 MB of HBM each); 0 = 1024 */
+                             1.7 MB of HBM each); 0 = 1024 */
 } at2v_queue_opts;
 #define AT2V_QUEUE_EAGER 1u
 #define AT2V_QUEUE_SENDER_COMB 2u /* the queue's context gets a sender cache (sender_cache keys) with sender_comb = 1 */

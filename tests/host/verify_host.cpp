@@ -107,24 +107,31 @@ struct HostTabBFu {
 
 // comb of one key (at2v_comb.h), built by comb_build_lane over all lanes exactly as the device's builders do
 struct HostComb {
-  std::vector<gu_cached> e;
+  std::vector<uint32_t> w;  // kCombPos x kCombEntries entries of kCombWords words (the device's payload layout)
   int a_ok = 0;
   mutable int pend[2] = {0, 0};
-  explicit HostComb(const uint32_t A[8]) : e((size_t)kCombPos * kCombEntries) {
+  explicit HostComb(const uint32_t A[8]) : w((size_t)kCombPos * kCombEntries * kCombWords) {
     // keys alternate between the device's two builder shapes (8 and 2 lanes per position, at2v_comb.h)
     if (A[0] & 1) build<kCombWideLog2>(A);
     else build<kCombNarrowLog2>(A);
   }
+  struct Mem {
+    uint32_t* row;
+    void put(int j, const uint32_t* src) const { std::memcpy(row + (size_t)j * kCombWords, src, kCombWords * 4); }
+    void get(int j, uint32_t* dst) const { std::memcpy(dst, row + (size_t)j * kCombWords, kCombWords * 4); }
+  };
   template <int kLog2>
   void build(const uint32_t A[8]) {
     for (int lane = 0; lane < (kCombPos << kLog2); ++lane) {
       const int pos = lane >> kLog2;
-      a_ok = comb_build_lane<kLog2>(A, pos, lane & ((1 << kLog2) - 1),
-                                    [&](int j, const gu_cached& c) { e[(size_t)pos * kCombEntries + j] = c; });
+      Mem mem{w.data() + (size_t)(pos < kCombPos ? pos : 0) * kCombEntries * kCombWords};
+      a_ok = comb_build_lane<kLog2>(A, pos, lane & ((1 << kLog2) - 1), mem);
     }
   }
   void prefetch(int st, int i, int j) const { pend[st] = i * kCombEntries + j; }
-  void load_prefetched(int st, gu_cached& c) const { c = e[pend[st]]; }
+  void load_prefetched(int st, CombEntry& c) const {
+    std::memcpy(&c, w.data() + (size_t)pend[st] * kCombWords, sizeof(CombEntry));
+  }
 };
 // D[i][j] = [j 2^(16 i)]B on demand: (j 2^(16 i)) mod l times B by the signed-field base ladder, then the unsigned form
 struct HostBComb {

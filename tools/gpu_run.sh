@@ -14,6 +14,7 @@
 #   torchrun1     the world-1 torchrun rehearsal of the N > 1 bench path (RCCL gather inside the timed loop)
 #   rocprof       rocprofv3 --kernel-trace --stats of a bench run with one scratch set (per-kernel averages)
 #   latency       tools/latency_probe.py --comb 1 (small-batch and first-seen-sender latency)
+#   latprof       rocprofv3 --kernel-trace of a short latency probe (per-launch kernel durations)
 #   fresh         tools/fresh_sweep.sh: config 5 with a stream of first-seen senders (queue p50/p99 per node)
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
 #   ab=<a,b,...>  tools/ab_bench.py over at2-node_amd/at2v/variants/libat2v_<a>.so ... (distinct keys)
@@ -60,6 +61,9 @@ for st in "$@"; do
                python3 bench.py --steps 20 --warmup 3 --pmc-traffic 0 --cpu-sample 0 --e2e 0
              unset AT2V_SCRATCH_SETS
              find $D/prof -name '*kernel_stats.csv' -exec cp {} $D/kernel_stats.csv \; ;;
+    latprof) run latprof 300 rocprofv3 --kernel-trace --output-format csv -d $D/latprof -o run -- \
+               python3 tools/latency_probe.py --reps 20 --comb 1 --sizes 1,64
+             find $D/latprof -name '*kernel_trace.csv' -exec cp {} $D/latprof_trace.csv \; ;;
     fresh) run fresh 900 bash tools/fresh_sweep.sh $TAG ;;
     pmc) run pmc 1100 bash tools/profile.sh $TAG ;;
     latency) run latency 400 python3 tools/latency_probe.py --reps 100 --comb 1

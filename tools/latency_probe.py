@@ -8,11 +8,13 @@ For batches of B records (default 1, 20, 64, 1024), each measured `--reps` times
   queue    : wall time from at2v_queue_submit of the B records to the last verdict polled (eager queue, idle,
              one batch in flight at a time);
   fresh    : (--comb 1) device time of launches whose B keys the context has never seen (steady state of a stream of
-             first-seen senders: the in-kernel lookup, then the two-wave half-size split);
-  first    : (--comb 1) device time of the FIRST launch of the B records in a fresh context, whose B keys are new:
-             the in-kernel lookup claims them and their chunks run the two-wave half-size split (the cost a first-seen
-             sender pays once; its comb is built afterwards on the context's build stream: `first_combs_ready_us` is
-             the wall time from that launch until at2v_get_info, which waits for the build stream, returns);
+             first-seen senders: the in-kernel lookup, then the four-wave split half-size check);
+  first    : (--comb 1) device time of a launch of B records whose keys a new context has not seen (after two such
+             launches of 64 other keys): the in-kernel lookup claims them and their chunks run the four-wave split
+             half-size check (the cost a first-seen sender pays once); the combs are built afterwards on the context's
+             own stream: `first_combs_ready_us` is the wall time from the launch until at2v_get_info returns;
+             `first_launch_shared_hw_queue_us` is a launch of 64 new keys on a stream that shares a hardware queue
+             with the context's stream (its end waits for the builds);
 reports p50/p90 per stage as JSON. Records come from the oracle generator (all valid), checked once per size."""
 import argparse
 import json
@@ -66,44 +68,38 @@ def main():
         first_us = None
         if a.comb:
             vc = at2v.BatchVerifier(device=0, sender_cache=1024, sender_comb=True)
-            # a running node's context: earlier launches (other keys, on the measured stream, both scratch sets) before
-            # the measured one, so the measurement is the first payload of new senders, not the first use of a new
-            # context (`first_launch_fresh_context_us`: these two launches, each after an idle pause)
-            wp, wg, wm, wf = o.gen_records(0x4154325F, 1 << 30, 128, a.msg_len)
+            # HIP maps a process's streams round robin onto GPU_MAX_HW_QUEUES (4) hardware queues. `ls`, created right
+            # after the context's own stream (where the combs are built), gets the next queue; `sh`, the fourth stream
+            # after it, wraps round to the context's queue: anything enqueued on sh after a launch waits for the comb
+            # build.
+            ls, _, _, sh = at2v.launch_streams(4)
+            # a running node's context: two earlier launches (other keys) before the measured one
+            wp, wg, wm, wf = o.gen_records(0x4154325F, 1 << 30, 3 * 64 + B, a.msg_len)
             wd = [torch.from_numpy(x.reshape(-1).copy()).cuda() for x in (wp, wg)]
             wdm = torch.from_numpy(np.concatenate([wm, np.zeros(16, np.uint8)])).cuda()
-            wv = torch.zeros(2, dtype=torch.int32, device="cuda")
-            fresh_ctx = []
-            for h in range(2):
-                wo = torch.from_numpy((wf[64 * h:64 * h + 65] - wf[64 * h]).view(np.int32).copy()).cuda()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
-                vc.verify_batch_device(wd[0].data_ptr() + 64 * h * 32, wd[1].data_ptr() + 64 * h * 64,
-                                       wdm.data_ptr() + int(wf[64 * h]), int(wf[64 * h + 64] - wf[64 * h]),
-                                       wo.data_ptr(), 64, wv.data_ptr(), s.cuda_stream)
-                e1.record(s)
+            wv = torch.zeros((B + 31) // 32 + 2, dtype=torch.int32, device="cuda")
+
+            def launch_new(lo, cnt, strm):
+                wo = torch.from_numpy((wf[lo:lo + cnt + 1] - wf[lo]).view(np.int32).copy()).cuda()
                 torch.cuda.synchronize()
-                fresh_ctx.append(e0.elapsed_time(e1) * 1e3)
-            vc.info()
-            torch.cuda.synchronize()
-            # a node's GPU is busy between payloads; after the host-side pauses above an idle GPU has dropped its clock,
-            # and a launch right then runs ~2.5x slower (first_launch_fresh_context_us). ~10 ms of other work on the
-            # same stream first, then the launch.
-            busy = torch.randn(4096, 4096, device="cuda")
-            for _ in range(8):
-                busy = busy @ busy
-                busy /= busy.abs().max()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            t_first = time.perf_counter()
-            e0.record(s)
-            vc.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), int(f[-1]), d_off.data_ptr(),
-                                   B, d_ver.data_ptr(), s.cuda_stream)
-            e1.record(s)
-            vc.info()  # waits for the build stream (combs of the B new keys)
-            combs_ready_us = (time.perf_counter() - t_first) * 1e6
-            torch.cuda.synchronize()
-            first_us = e0.elapsed_time(e1) * 1e3
-            assert (d_ver.cpu().numpy().view(np.uint32)[: B // 32] == 0xFFFFFFFF).all()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t = time.perf_counter()
+                e0.record(strm)
+                vc.verify_batch_device(wd[0].data_ptr() + lo * 32, wd[1].data_ptr() + lo * 64,
+                                       wdm.data_ptr() + int(wf[lo]), int(wf[lo + cnt] - wf[lo]), wo.data_ptr(), cnt,
+                                       wv.data_ptr(), strm.cuda_stream)
+                e1.record(strm)
+                e1.synchronize()
+                dev_us = e0.elapsed_time(e1) * 1e3
+                vc.info()  # waits for the context's stream (the combs of the new keys)
+                ready_us = (time.perf_counter() - t) * 1e6
+                ok = (wv.cpu().numpy().view(np.uint32)[: cnt // 32] == 0xFFFFFFFF).all()
+                assert ok
+                return dev_us, ready_us
+
+            warm = [launch_new(0, 64, ls)[0], launch_new(64, 64, ls)[0]]
+            first_us, combs_ready_us = launch_new(128, B, ls)
+            shared_us, _ = launch_new(128 + B, 64, sh)
             vc.close()
         fresh = []
         if a.comb and a.fresh_reps:
@@ -152,7 +148,8 @@ def main():
         if first_us is not None:
             out["sizes"][B]["first_launch_new_keys_us"] = first_us
             out["sizes"][B]["first_combs_ready_us"] = combs_ready_us
-            out["sizes"][B]["first_launch_fresh_context_us"] = fresh_ctx
+            out["sizes"][B]["warm_launches_new_keys_us"] = warm
+            out["sizes"][B]["first_launch_shared_hw_queue_us"] = shared_us
         print(B, json.dumps(out["sizes"][B]), file=sys.stderr)
     q.close()
     v.close()
