@@ -232,10 +232,11 @@ def check_group_law(C, K):
     d2 = add(C, C)
     Gm = add(d2, C); Fm = pcarry_even(add(d2, KC))
     madd = (Ea, Ha, Gm, Fm)
-    # p1p1 (X, Y, Z, T) -> p2 / p3 (gu_p1p1_to_p2 / _p3): X3 = X T (wide), Y3 = Y Z (narrow), Z3 = Z T (wide),
-    # T3 = X Y (wide)
+    # p1p1 (X, Y, Z, T) -> p2 / p3 (gu_p1p1_to_p2 / _p3): X3 = X T (wide), Y3 = Y Z or Z Y (AT2V_GU_SHARE; narrow),
+    # Z3 = Z T (wide), T3 = X Y (wide)
     for (x, y, z, t), nm in ((dbl, "dbl"), (addr, "add"), (madd, "madd")):
-        m.mul(x, t, nm + " X"); m.mul(y, z, nm + " Y", True); m.mul(z, t, nm + " Z"); m.mul(x, y, nm + " T")
+        m.mul(x, t, nm + " X"); m.mul(y, z, nm + " Y", True); m.mul(z, y, nm + " Y'", True)
+        m.mul(z, t, nm + " Z"); m.mul(x, y, nm + " T")
     # --- cached form of a p3 point: YpX = Y + X, YmX = Y + K_C - X, Z2 = 2Z, T2d = T * 2d
     m.mul(C, C, "T2d", True)
     # --- decode: u = y^2 + (p - 1), v = d y^2 + 1; checks on v x^2 -+ u
