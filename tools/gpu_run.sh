@@ -12,6 +12,7 @@
 #   bench         python bench.py (the default driver line: config 2 + at2_traffic + roofline + cpu_baseline)
 #   bench1        python bench.py with the PMC passes and CPU baseline off (a quick rate check)
 #   torchrun1     the world-1 torchrun rehearsal of the N > 1 bench path (RCCL gather inside the timed loop)
+#   torchrun3     the same with config 3's per-rank load (2M records per rank: 16M over 8 GPUs)
 #   rocprof       rocprofv3 --kernel-trace --stats of a bench run with one scratch set (per-kernel averages)
 #   latency       tools/latency_probe.py --comb 1 (small-batch and first-seen-sender latency)
 #   latprof       rocprofv3 --kernel-trace of a short latency probe (per-launch kernel durations)
@@ -56,6 +57,9 @@ for st in "$@"; do
     torchrun1) run torchrun1 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
                  --master-port 29533 bench.py --gpus 1 --steps 10 --warmup 2 --e2e 0
                grep '^{' $D/torchrun1.txt > $D/torchrun1.json ;;
+    torchrun3) run torchrun3 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+                 --master-port 29534 bench.py --gpus 1 --steps 10 --warmup 2 --e2e 0 --records-per-gpu 2097152
+               grep '^{' $D/torchrun3.txt > $D/torchrun3.json ;;
     rocprof) export AT2V_SCRATCH_SETS=1
              run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- \
                python3 bench.py --steps 20 --warmup 3 --pmc-traffic 0 --cpu-sample 0 --e2e 0
