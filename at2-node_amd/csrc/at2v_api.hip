@@ -287,12 +287,17 @@ hipError_t cache_before_launch(SenderCache& c, hipStream_t stream, int j) {
   return e;
 }
 
-// The builds of a cached launch's claim slot (build stream: after the launch, payloads, flip, slot free).
+// The builds of a cached launch's claim slot (build stream: after the launch, payloads, flip, slot free), then the
+// counters' copy for the host (the compaction check of a later launch reads kCtlFull from it): on the context's stream,
+// so the caller's stream carries only the verify kernel.
 hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
   hipError_t e = hipStreamWaitEvent(c.build, c.claims_ready[b.slot], 0);
   if (e == hipSuccess) e = at2v::launch_cache_build(b.args, b.max_claims, c.build);
   if (e == hipSuccess) e = hipEventRecord(c.slot_free[b.slot], c.build);
   if (e == hipSuccess) e = hipEventRecord(c.built, c.build);
+  if (e == hipSuccess) e = hipMemcpyAsync(c.host_ctl, c.ctl.p, c.ctl.cap, hipMemcpyDeviceToHost, c.build);
+  if (e == hipSuccess) e = hipEventRecord(c.ctl_copied, c.build);
+  c.copy_pending = e == hipSuccess;
   return e;
 }
 
@@ -339,9 +344,6 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
       if (defer_build) c->deferred = b;  // the caller enqueues it after its own work on the shard stream
       else e = enqueue_cache_build(*c, b);
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(c->host_ctl, c->ctl.p, c->ctl.cap, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipEventRecord(c->ctl_copied, stream);
-    c->copy_pending = e == hipSuccess;
   }
   if (e == hipSuccess) e = hipEventRecord(s.scratch_free[j], stream);
   return e;

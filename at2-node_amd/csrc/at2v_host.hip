@@ -7,6 +7,8 @@
 //   * at2v_ledger_*  accounts / recent transactions / apply loop (at2v_ledger.h).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -36,6 +38,13 @@ struct HipBackend {
   // (GPU_MAX_HW_QUEUES = 4), so no verify or copy of the latency path waits behind a comb build in a shared queue
   hipStream_t h2d = nullptr, comp[2] = {nullptr, nullptr};
   unsigned launches = 0;
+  // the kernel writes the verdict words straight into the slot's pinned host words (no device-to-host copy after the
+  // kernel: one dependent copy less on the latency path); AT2V_QUEUE_DIRECT=0 restores the copy (A/B)
+  bool direct = true;
+  // latency mode (eager): the completer polls the batch's event for up to spin_us before a blocking wait, so a verdict
+  // is seen within ~1 us of the kernel's end instead of after a blocking-wait wake-up (AT2V_QUEUE_SPIN_US overrides;
+  // 0 = always the blocking wait). Costs one host core while a batch is in flight.
+  uint32_t spin_us = 0;
 
   int init(const at2v_queue_opts& o) {
     at2v_opts co{o.device, 1, o.policy, 0, 0, 0};
@@ -46,6 +55,9 @@ struct HipBackend {
     const int rc = at2v_create(&co, &ctx);
     if (rc) return rc;
     device = o.device;
+    if (const char* v = std::getenv("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
+    spin_us = (o.flags & AT2V_QUEUE_EAGER) ? 2000u : 0u;
+    if (const char* v = std::getenv("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
     if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
     if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     for (hipStream_t& c : comp)
@@ -107,7 +119,8 @@ struct HipBackend {
     delete d;
     s.backend = nullptr;
   }
-  // H2D on h2d -> verify on comp[k % 2] (waits for its upload) -> D2H on the same comp stream
+  // H2D on h2d -> verify on comp[k % 2] (waits for its upload), verdict words written to pinned host memory (or a D2H
+  // copy on the same comp stream with AT2V_QUEUE_DIRECT=0)
   int launch(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
     hipStream_t comp = this->comp[launches++ & 1];
@@ -124,15 +137,30 @@ struct HipBackend {
     if (e == hipSuccess) e = hipEventRecord(d->uploaded, h2d);
     if (e == hipSuccess) e = hipStreamWaitEvent(comp, d->uploaded, 0);
     if (e != hipSuccess) return AT2V_E_HIP;
+    uint32_t* ver = direct ? s.verdicts : (uint32_t*)d->ver;
     const int rc = at2v_verify_batch_device(ctx, (const uint8_t*)d->pk, (const uint8_t*)d->sig, (const uint8_t*)d->msg,
-                                            s.msg_used, (const uint32_t*)d->off, n, (uint32_t*)d->ver, comp);
+                                            s.msg_used, (const uint32_t*)d->off, n, ver, comp);
     if (rc) return rc;
-    e = hipMemcpyAsync(s.verdicts, d->ver, words * 4, hipMemcpyDeviceToHost, comp);
+    if (!direct) e = hipMemcpyAsync(s.verdicts, d->ver, words * 4, hipMemcpyDeviceToHost, comp);
     if (e == hipSuccess) e = hipEventRecord(d->done, comp);
     return e == hipSuccess ? AT2V_OK : AT2V_E_HIP;
   }
   int wait(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
+    if (spin_us) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned k = 0;; ++k) {
+        const hipError_t q = hipEventQuery(d->done);
+        if (q == hipSuccess) return AT2V_OK;
+        if (q != hipErrorNotReady) return AT2V_E_HIP;
+        if ((k & 63) == 63 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
+          break;
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+    }
     return hipEventSynchronize(d->done) == hipSuccess ? AT2V_OK : AT2V_E_HIP;
   }
 };

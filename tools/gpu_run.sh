@@ -15,6 +15,9 @@
 #   torchrun3     the same with config 3's per-rank load (2M records per rank: 16M over 8 GPUs)
 #   rocprof       rocprofv3 --kernel-trace --stats of a bench run with one scratch set (per-kernel averages)
 #   latency       tools/latency_probe.py --comb 1 (small-batch and first-seen-sender latency)
+#   latab         latency probe and config 5 (combs) with the queue's verdict copy (AT2V_QUEUE_DIRECT=0) and with direct
+#                 verdict writes (=1), alternating
+#   spinab        the same A/B for the completer's event polling (AT2V_QUEUE_SPIN_US=0 vs 2000)
 #   latprof       rocprofv3 --kernel-trace of a short latency probe (per-launch kernel durations)
 #   fresh         tools/fresh_sweep.sh: config 5 with a stream of first-seen senders (queue p50/p99 per node)
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
@@ -65,6 +68,16 @@ for st in "$@"; do
                python3 bench.py --steps 20 --warmup 3 --pmc-traffic 0 --cpu-sample 0 --e2e 0
              unset AT2V_SCRATCH_SETS
              find $D/prof -name '*kernel_stats.csv' -exec cp {} $D/kernel_stats.csv \; ;;
+    latab) for r in 1 2; do for v in 0 1; do
+             AT2V_QUEUE_DIRECT=$v run lat_d${v}_$r 300 python3 tools/latency_probe.py --reps 100 --comb 1 --sizes 1,20,64
+             AT2V_QUEUE_DIRECT=$v run c5_d${v}_$r 200 python3 tools/mininode.py --nodes 4 --rate 20000 --seconds 2 \
+               --batch 1024 --delay-us 1000 --eager 1 --comb 1
+           done; done ;;
+    spinab) for r in 1 2; do for v in 0 2000; do
+             AT2V_QUEUE_SPIN_US=$v run lat_s${v}_$r 300 python3 tools/latency_probe.py --reps 100 --comb 1 --sizes 1,20,64
+             AT2V_QUEUE_SPIN_US=$v run c5_s${v}_$r 200 python3 tools/mininode.py --nodes 4 --rate 20000 --seconds 2 \
+               --batch 1024 --delay-us 1000 --eager 1 --comb 1
+           done; done ;;
     latprof) run latprof 300 rocprofv3 --kernel-trace --output-format csv -d $D/latprof -o run -- \
                python3 tools/latency_probe.py --reps 20 --comb 1 --sizes 1,64
              find $D/latprof -name '*kernel_trace.csv' -exec cp {} $D/latprof_trace.csv \; ;;
