@@ -41,9 +41,8 @@ struct HipBackend {
   // the kernel writes the verdict words straight into the slot's pinned host words (no device-to-host copy after the
   // kernel: one dependent copy less on the latency path); AT2V_QUEUE_DIRECT=0 restores the copy (A/B)
   bool direct = true;
-  // latency mode (eager): the completer polls the batch's event for up to spin_us before a blocking wait, so a verdict
-  // is seen within ~1 us of the kernel's end instead of after a blocking-wait wake-up (AT2V_QUEUE_SPIN_US overrides;
-  // 0 = always the blocking wait). Costs one host core while a batch is in flight.
+  // AT2V_QUEUE_SPIN_US > 0: the completer polls the batch's event for up to that long before the blocking wait. Off:
+  // on MI355X the blocking wait already returns as fast (config 5 queue p50 within 2 us either way, profiles/r04v).
   uint32_t spin_us = 0;
 
   int init(const at2v_queue_opts& o) {
@@ -56,7 +55,6 @@ struct HipBackend {
     if (rc) return rc;
     device = o.device;
     if (const char* v = std::getenv("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
-    spin_us = (o.flags & AT2V_QUEUE_EAGER) ? 2000u : 0u;
     if (const char* v = std::getenv("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
     if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
     if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
