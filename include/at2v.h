@@ -204,7 +204,9 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
  * its oldest record is max_delay_us old, or on at2v_queue_flush() — and, with AT2V_QUEUE_EAGER, whenever
  * no batch is in flight (latency mode) — and verified on the GPU asynchronously (depth slots: one
  * filling, up to depth-1 in flight). Verdicts come back in ticket
- * (= submission) order. Thread-safe: any number of producer threads; poll from any thread. */
+ * (= submission) order. Thread-safe: any number of producer threads; poll from any thread.
+ * A slot's records live in pinned host memory: a batch of up to 1,024 records is read by the kernel from there, a
+ * larger one is uploaded first; the kernel writes the verdict words straight into pinned host memory. */
 typedef struct at2v_queue at2v_queue;
 typedef struct {
   int device;             /* HIP device ordinal */
