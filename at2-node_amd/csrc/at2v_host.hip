@@ -201,6 +201,7 @@ int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (o.max_msg_bytes) qo.max_msg_bytes = o.max_msg_bytes;
   if (o.depth) qo.depth = (int)o.depth;
   qo.eager = (o.flags & AT2V_QUEUE_EAGER) != 0;
+  if (const char* v = std::getenv("AT2V_QUEUE_LAUNCH_HERE")) qo.launch_here = std::atoi(v) != 0;  // (A/B)
   if (o.flags & ~(AT2V_QUEUE_EAGER | AT2V_QUEUE_SENDER_COMB)) return AT2V_E_INVALID;
   if (qo.depth < 2 || qo.max_batch >= (1u << 31) || (uint64_t)qo.max_batch * qo.max_msg_bytes >= (1ull << 32))
     return AT2V_E_INVALID;

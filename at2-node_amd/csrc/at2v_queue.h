@@ -40,6 +40,7 @@ struct QueueOpts {
   size_t max_msg_bytes = 256;  // average message bytes budgeted per record (slot msg capacity = max_batch x this)
   int depth = 3;               // slots: 1 filling + up to depth-1 in flight
   bool eager = false;          // also seal whenever the device is idle (no batch in flight)
+  bool launch_here = true;     // eager: the producer / completer that finds the device idle launches the batch itself
 };
 
 struct QueueSlot {
@@ -166,6 +167,12 @@ class BatchQueue {
       i += m;
       if (s.n == s.cap_records) seal_locked();
     }
+    // latency mode with the device idle: this thread seals and launches the batch itself instead of waking the
+    // launcher thread (one thread hand-off less per lone batch); if a launch is under way the launcher takes it
+    if (o_.eager && o_.launch_here && fill_ && fill_->n && ready_.empty() && inflight_.empty() && !launching_) {
+      seal_locked();
+      launch_here_locked(lk);
+    }
     return 0;
   }
 
@@ -238,6 +245,29 @@ class BatchQueue {
     cv_launch_.notify_all();
   }
 
+  // Launch the oldest sealed batch. Caller holds m_ (lk) and launch_m_; m_ is released around the backend call. Every
+  // launch runs under launch_m_ and pops/pushes under m_, so launch order = seal order = ticket order whichever
+  // thread launches.
+  void launch_one_locked(std::unique_lock<std::mutex>& lk) {
+    QueueSlot* s = ready_.front();
+    ready_.pop_front();
+    ++launching_;
+    lk.unlock();
+    s->status = be_.launch(*s);
+    lk.lock();
+    --launching_;
+    inflight_.push_back(s);
+    cv_complete_.notify_all();
+  }
+
+  // From a producer or the completer (holding m_): launch what is sealed if no other thread is launching; never
+  // blocks on launch_m_ while holding m_ (the launcher thread takes launch_m_ before m_).
+  void launch_here_locked(std::unique_lock<std::mutex>& lk) {
+    if (ready_.empty() || !launch_m_.try_lock()) return;
+    std::lock_guard<std::mutex> g(launch_m_, std::adopt_lock);
+    while (!ready_.empty()) launch_one_locked(lk);
+  }
+
   void launcher_loop() {
     std::unique_lock<std::mutex> lk(m_);
     while (true) {
@@ -247,15 +277,10 @@ class BatchQueue {
       }
       if (flush_req_ && (!fill_ || fill_->n == 0)) flush_req_ = false;
       if (!ready_.empty()) {
-        QueueSlot* s = ready_.front();
-        ready_.pop_front();
-        ++launching_;
         lk.unlock();
-        s->status = be_.launch(*s);
+        std::lock_guard<std::mutex> g(launch_m_);  // (launch_m_ before m_: see launch_here_locked)
         lk.lock();
-        --launching_;
-        inflight_.push_back(s);  // only this thread launches: launch order == seal order == ticket order
-        cv_complete_.notify_all();
+        if (!ready_.empty()) launch_one_locked(lk);
         continue;
       }
       if (!running_) break;
@@ -298,7 +323,12 @@ class BatchQueue {
       free_.push_back(s);
       cv_free_.notify_all();
       cv_done_.notify_all();
-      if (o_.eager) cv_launch_.notify_all();  // the device went idle: seal what is filling
+      if (o_.eager && o_.launch_here && fill_ && fill_->n && ready_.empty() && inflight_.empty() && !launching_) {
+        seal_locked();  // the device went idle: seal what is filling and launch it from here
+        launch_here_locked(lk);
+      } else if (o_.eager) {
+        cv_launch_.notify_all();
+      }
       if ((!fill_ || fill_->n == 0) && ready_.empty() && !launching_ && inflight_.empty()) cv_idle_.notify_all();
     }
   }
@@ -315,7 +345,7 @@ class BatchQueue {
   uint64_t next_ticket_ = 0;
   int launching_ = 0;
   bool running_ = false, flush_req_ = false;
-  std::mutex m_, submit_m_;
+  std::mutex m_, submit_m_, launch_m_;
   std::condition_variable cv_launch_, cv_complete_, cv_free_, cv_done_, cv_idle_;
   std::thread launcher_, completer_;
 };

@@ -1,7 +1,7 @@
 // queue_host.cpp — TEST ONLY: the product's batching queue (at2-node_amd/csrc/at2v_queue.h) driven on
 // the CPU with the oracle as its verify backend, to check flush policy, ticket order and verdict mapping
 // without a GPU. The shipped queue is instantiated with the HIP backend in at2v_host.hip.
-// usage: queue_host <scenario>   scenario in {order, size, deadline, flush, eager, drain, startfail, failed}; exit 0 = pass
+// usage: queue_host <scenario>   scenario in {order, size, deadline, flush, eager, eager_order, drain, startfail, failed}; exit 0 = pass
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -236,6 +236,54 @@ int scenario_eager() {
   return 0;
 }
 
+int scenario_eager_order() {
+  // eager mode with 4 producers: batches are launched by producers, the completer and the launcher thread alike;
+  // tickets still map back to records and verdicts come back in ticket order
+  Records r(3000, 61);
+  OracleBackend be;
+  QueueOpts o;
+  o.max_batch = 256;
+  o.max_delay_us = 30000000;
+  o.max_msg_bytes = 64;
+  o.depth = 3;
+  o.eager = true;
+  BatchQueue<OracleBackend> q(be, o);
+  REQUIRE(q.start() == 0);
+  std::vector<uint64_t> ticket_of(r.n, UINT64_MAX);
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (int p = 0; p < 4; ++p)
+    th.emplace_back([&, p] {
+      std::mt19937 rng(100 + p);
+      while (true) {
+        const size_t len = 1 + rng() % 9;
+        const size_t a = next.fetch_add(len);
+        if (a >= r.n) break;
+        const size_t m = std::min(len, r.n - a);
+        std::vector<uint32_t> off(m + 1);
+        for (size_t i = 0; i <= m; ++i) off[i] = (uint32_t)(i * r.L);
+        uint64_t first;
+        if (q.submit(&r.pk[32 * a], &r.sig[64 * a], &r.msg[r.L * a], off.data(), m, &first) != 0) abort();
+        for (size_t i = 0; i < m; ++i) ticket_of[a + i] = first + i;
+      }
+    });
+  for (auto& t : th) t.join();
+  std::vector<uint8_t> got(r.n, 0xee);
+  std::vector<uint64_t> order;
+  REQUIRE(drain(q, got, order, r.n, 60000000) == (long)r.n);
+  for (size_t i = 0; i < order.size(); ++i) REQUIRE(order[i] == i);
+  size_t bad = 0;
+  for (size_t i = 0; i < r.n; ++i) {
+    REQUIRE(ticket_of[i] != UINT64_MAX);
+    bad += got[ticket_of[i]] != r.want[i];
+  }
+  const QueueStats s = q.stats();
+  printf("eager_order n=%zu mismatches=%zu batches=%llu mean_batch=%.1f\n", r.n, bad, (unsigned long long)s.batches,
+         s.mean_batch);
+  REQUIRE(bad == 0 && s.completed == r.n && s.batches > 1);
+  return 0;
+}
+
 int scenario_flush() {
   Records r(5, 32);
   OracleBackend be;
@@ -334,6 +382,7 @@ int main(int argc, char** argv) {
   if (!strcmp(s, "deadline")) return scenario_deadline();
   if (!strcmp(s, "flush")) return scenario_flush();
   if (!strcmp(s, "eager")) return scenario_eager();
+  if (!strcmp(s, "eager_order")) return scenario_eager_order();
   if (!strcmp(s, "drain")) return scenario_drain();
   if (!strcmp(s, "startfail")) return scenario_startfail();
   if (!strcmp(s, "failed")) return scenario_failed();

@@ -100,11 +100,12 @@ def queue_host():
 
 
 @pytest.mark.parametrize("build", list(SANITIZE))
-@pytest.mark.parametrize("scenario", ["order", "size", "deadline", "flush", "eager", "drain", "startfail", "failed"])
+@pytest.mark.parametrize("scenario", ["order", "size", "deadline", "flush", "eager", "eager_order", "drain", "startfail", "failed"])
 def test_queue_core_on_host(queue_host, scenario, build):
     """order: 4 producer threads, random run lengths, verdicts map back through tickets (oracle backend);
     size: a full batch seals at max_batch; deadline: a partial batch seals at max_delay_us;
-    flush: explicit seal, oversized message rejected; drain: destroy completes everything submitted;
+    flush: explicit seal, oversized message rejected; eager_order: latency mode with 4 producers, batches launched by
+    producers, the completer and the launcher thread, ticket order kept; drain: destroy completes everything submitted;
     startfail: a start() that fails part-way frees every slot; failed: a batch whose launch fails
     reports 0xff for its records and is counted in failed_batches. Each under ASan+UBSan and TSan too."""
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",

@@ -19,6 +19,7 @@
 #                 verdict writes (=1), alternating
 #   spinab        the same A/B for the completer's event polling (AT2V_QUEUE_SPIN_US=0 vs 2000)
 #   zcab          the same A/B for kernels reading small batches from pinned host memory (AT2V_QUEUE_ZEROCOPY=0 vs 1024)
+#   lhab          the same A/B for launches from the producer / completer thread (AT2V_QUEUE_LAUNCH_HERE=0 vs 1)
 #   latprof       rocprofv3 --kernel-trace of a short latency probe (per-launch kernel durations)
 #   fresh         tools/fresh_sweep.sh: config 5 with a stream of first-seen senders (queue p50/p99 per node)
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
@@ -82,6 +83,11 @@ for st in "$@"; do
     zcab) for r in 1 2; do for v in 0 1024; do
              AT2V_QUEUE_ZEROCOPY=$v run lat_z${v}_$r 300 python3 tools/latency_probe.py --reps 100 --comb 1 --sizes 1,64,1024
              AT2V_QUEUE_ZEROCOPY=$v run c5_z${v}_$r 200 python3 tools/mininode.py --nodes 4 --rate 20000 --seconds 2 \
+               --batch 1024 --delay-us 1000 --eager 1 --comb 1
+           done; done ;;
+    lhab) for r in 1 2; do for v in 0 1; do
+             AT2V_QUEUE_LAUNCH_HERE=$v run lat_l${v}_$r 300 python3 tools/latency_probe.py --reps 100 --comb 1 --sizes 1,20,64
+             AT2V_QUEUE_LAUNCH_HERE=$v run c5_l${v}_$r 200 python3 tools/mininode.py --nodes 4 --rate 20000 --seconds 2 \
                --batch 1024 --delay-us 1000 --eager 1 --comb 1
            done; done ;;
     latprof) run latprof 300 rocprofv3 --kernel-trace --output-format csv -d $D/latprof -o run -- \
