@@ -291,7 +291,9 @@ def main():
     total = n * world * args.steps
     value = total / elapsed
     per_gpu_kernel_rate = n / (kernel_ms * 1e-3)
-    achieved = per_gpu_kernel_rate * MAC_PER_VERIFY / 1e12
+    # the comb path (repeating senders with combs as the main leg) does far fewer MACs per verify than the ladder
+    macs = COMB_MAC_PER_VERIFY if (args.senders and args.sender_cache and args.sender_comb) else MAC_PER_VERIFY
+    achieved = per_gpu_kernel_rate * macs / 1e12
     info = v.info()
 
     out = None
@@ -347,7 +349,7 @@ def main():
                 "unit": "Tops/s (32x32->64 integer MAC, v_mad_u64_u32)",
                 "frac": achieved * 1e12 / MAC_PEAK,
                 "traffic": None,
-                "alg_macs_per_verify": MAC_PER_VERIFY,
+                "alg_macs_per_verify": macs,
                 "alg_bytes_per_verify": 32 + 64 + L + 4,
                 # algorithmic input rate (records x 200 B / kernel time); the measured memory-side rate from the
                 # PMC counters is hbm_gbs (filled below at N = 1 when the counter passes run)
@@ -598,7 +600,8 @@ def _pmc_pass(args, n, L, counters):
         return None
     d = tempfile.mkdtemp(prefix="at2v_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", *counters, "--kernel-trace", "--output-format", "csv",
-           "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "0",
+           "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "2",
+           "--warmup", "2" if args.senders else "0",  # repeating senders: the keys are cached by the profiled steps
            "--cpu-sample", "0", "--pmc-traffic", "0", "--records-per-gpu", str(n), "--msg-len", str(L),
            "--policy", args.policy, "--senders", str(args.senders), "--sender-cache", str(args.sender_cache),
            "--sender-comb", str(args.sender_comb), "--e2e", "0", "--traffic-leg", "0"]
@@ -618,11 +621,15 @@ def _pmc_pass(args, n, L, counters):
             per = {}
             for r in rows:  # one row per dispatch (and per agent/XCD if split): sum by dispatch
                 if r["Counter_Name"] == ctr:
-                    k = r.get("Dispatch_Id", "0")
+                    k = int(r.get("Dispatch_Id", "0"))
                     per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
             if not per:
                 return None
+            if args.senders:  # the two timed steps only (the warm-up launches claim and build the keys)
+                per = {k: per[k] for k in sorted(per)[-2:]}
             out[ctr] = sum(per.values()) / len(per)
+        if args.senders:
+            durs = durs[-2:]
         return out, (sum(durs) / len(durs) if durs else None)
     except (subprocess.SubprocessError, OSError, KeyError, ValueError):
         return None

@@ -10,6 +10,7 @@
 #                 failure (time limit, crash) does
 #   smoke         __graft_entry__.smoke()
 #   bench         python bench.py (the default driver line: config 2 + at2_traffic + roofline + cpu_baseline)
+#   benchat2      python bench.py on AT2 traffic as the main leg (64 senders, combs) with the PMC passes
 #   bench1        python bench.py with the PMC passes and CPU baseline off (a quick rate check)
 #   torchrun1     the world-1 torchrun rehearsal of the N > 1 bench path (RCCL gather inside the timed loop)
 #   torchrun3     the same with config 3's per-rank load (2M records per rank: 16M over 8 GPUs)
@@ -57,6 +58,8 @@ for st in "$@"; do
     smoke) run smoke 180 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 500 python3 bench.py
            grep '^{' $D/bench.txt > $D/bench.json ;;
+    benchat2) run benchat2 400 python3 bench.py --senders 64 --sender-cache 1024 --sender-comb 1 --cpu-sample 0 --e2e 0
+              grep '^{' $D/benchat2.txt > $D/benchat2.json ;;
     bench1) run bench1 300 python3 bench.py --pmc-traffic 0 --cpu-sample 0 --e2e 0
             grep '^{' $D/bench1.txt > $D/bench1.json ;;
     torchrun1) run torchrun1 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
