@@ -904,6 +904,12 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
 template <class Body>
 __device__ AT2V_INLINE int with_msg_reader(const uint8_t* __restrict__ msg, uint32_t msg_total, uint32_t b0, uint32_t bl,
                                            Body&& body) {
+#if AT2V_EXP_CONST_MSG  // EXPERIMENT (wrong verdicts, timing only): message words from registers, no message loads
+  auto msg_const = [=](uint32_t j) -> uint32_t { return j * 0x01010101u + b0; };
+  auto touched0 = [] {};
+  MsgSplit<decltype(msg_const), decltype(msg_const), decltype(touched0)> mc{1, msg_const, msg_const, touched0};
+  return body(mc);
+#endif
   const int msg_fast = __builtin_amdgcn_readfirstlane(__all((uint64_t)b0 + bl + 8 <= (uint64_t)msg_total) ? 1 : 0);
   const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg) + (b0 >> 2);
   const uint32_t msh = (b0 & 3u) * 8;
