@@ -246,6 +246,10 @@ struct DevComb {
   int lane;
   __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's previous entry has been read out
+#if AT2V_EXP_COMB_HOT  // EXPERIMENT (wrong verdicts, timing only): every A entry read is the same cache-hot line
+    i = 0;
+    j = 1;
+#endif
     const int4* src = base + ((size_t)i * kCombEntries + j) * kCombGranules;
 #pragma unroll
     for (int q = 0; q < kCombGranules; ++q)
@@ -275,6 +279,10 @@ struct DevBComb {
   int lane;
   __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if AT2V_EXP_COMB_HOT
+    i = 0;
+    j = 1;
+#endif
     const int4* src = base + ((size_t)i * kBCombEntries + j) * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
