@@ -80,7 +80,7 @@ def test_config1_traffic_every_chunk_hits(at2v_mod, oracle, comb):
 def test_golden_sets_with_cache(at2v_mod, golden, policy, comb):
     """every golden fixture set, twice (cold, then warm cache), both policies: the small-order, non-canonical and
     off-curve senders of the adversarial/edge sets are cached with their decode verdicts"""
-    # 16,384 keys hold every set's senders (<= 9,200 distinct); with combs that is 16,384 x 2.1 MB = 35 GB of HBM
+    # 16,384 keys hold every set's senders (<= 9,200 distinct); with combs that is 16,384 x 1.7 MB = 28 GB of HBM
     with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 14, sender_comb=comb) as v:
         for name in golden_io.SETS:
             g = golden[name]
@@ -324,3 +324,44 @@ def test_comb_small_and_ragged_launches(at2v_mod, oracle, n):
             assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
             info = v.info()
         assert info["cache_chunk_hits"] > 0
+
+
+@pytest.mark.parametrize("n", [2048, 40000])
+def test_device_launches_while_combs_build(at2v_mod, oracle, golden, n):
+    """VERDICT r3 "Next" 4, the chunks whose comb is still building: device launches on a caller stream go back to back,
+    so the second and third launch of the same records start while the context's stream may still be building the
+    combs the first launch claimed. Their chunks then find entries that are claimed but not valid and fall back to the
+    half-size check. n = 2048: the four-wave kernel; n = 40000: the four-records-per-lane throughput kernel. Records
+    from 64 senders with every fourth one mutated (oracle verdicts), plus the adversarial golden set the same way."""
+    import torch
+    rng = np.random.default_rng(n)
+    pk, sig, msg, off = _gen_senders(at2v_mod, n, 100, 64)
+    sig = sig.copy()
+    bad = rng.choice(n, n // 4, replace=False)
+    sig[bad, 3] ^= 0x10  # R changes: those records must be rejected
+    want = oracle.verify_batch(pk, sig, msg, off)
+    g = golden["adversarial"]
+    sets = [(pk, sig, msg, off, want), (g.pk, g.sig, g.msg, g.off, g.dalek)]
+    stream = torch.cuda.Stream()
+    for (p_, s_, m_, o_, w_) in sets:
+        m = len(p_)
+        with at2v_mod.BatchVerifier(sender_cache=1024, sender_comb=True) as v:
+            d = [torch.from_numpy(np.ascontiguousarray(x).reshape(-1)).cuda() for x in (p_, s_)]
+            d_msg = torch.from_numpy(np.concatenate([m_, np.zeros(16, np.uint8)])).cuda()
+            d_off = torch.from_numpy(np.ascontiguousarray(o_).view(np.int32)).cuda()
+            outs = [torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda") for _ in range(3)]
+            torch.cuda.synchronize()
+            for o in outs:  # back to back on one caller stream: no wait for the context's comb builds
+                v.verify_batch_device(d[0].data_ptr(), d[1].data_ptr(), d_msg.data_ptr(), int(o_[-1]), d_off.data_ptr(),
+                                      m, o.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            for k, o in enumerate(outs):
+                got = at2v_mod.unpack_verdicts(o.cpu().numpy().view(np.uint32), m)
+                assert np.array_equal(got, w_), (m, k, np.nonzero(got != w_)[0][:10])
+            v.info()  # combs built: a fourth launch takes the comb path where every key is cached
+            last = torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda")
+            v.verify_batch_device(d[0].data_ptr(), d[1].data_ptr(), d_msg.data_ptr(), int(o_[-1]), d_off.data_ptr(), m,
+                                  last.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            got = at2v_mod.unpack_verdicts(last.cpu().numpy().view(np.uint32), m)
+            assert np.array_equal(got, w_)
