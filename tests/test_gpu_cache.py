@@ -346,9 +346,9 @@ def test_device_launches_while_combs_build(at2v_mod, oracle, golden, n):
     for (p_, s_, m_, o_, w_) in sets:
         m = len(p_)
         with at2v_mod.BatchVerifier(sender_cache=1024, sender_comb=True) as v:
-            d = [torch.from_numpy(np.ascontiguousarray(x).reshape(-1)).cuda() for x in (p_, s_)]
+            d = [torch.from_numpy(np.array(x, copy=True).reshape(-1)).cuda() for x in (p_, s_)]
             d_msg = torch.from_numpy(np.concatenate([m_, np.zeros(16, np.uint8)])).cuda()
-            d_off = torch.from_numpy(np.ascontiguousarray(o_).view(np.int32)).cuda()
+            d_off = torch.from_numpy(np.array(o_, copy=True).view(np.int32)).cuda()
             outs = [torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda") for _ in range(3)]
             torch.cuda.synchronize()
             for o in outs:  # back to back on one caller stream: no wait for the context's comb builds
