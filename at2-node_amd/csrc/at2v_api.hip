@@ -71,12 +71,11 @@ struct DevBuf {
 };
 
 // Per-sender A cache of one device (at2v_opts.sender_cache; at2v_cache.h). Cached launch L claims new keys
-// into claim slot b = L % kClaimSlots; right after the launch the build stream builds the slot's payloads, flips them
-// valid and frees the slot (slot_free[b]), so no launch waits for a build unless kClaimSlots launches in a row are
-// still waiting for theirs. (The claim slots were round 4's first design's claim sets plus build slots and a copy kernel
-// between them; a copy queued on the build stream behind a 0.8 ms comb build stalled the latency path just the same.)
-// When a launch finds the free list empty, the host learns it from the counters' asynchronous copy and compacts the
-// cache before a later launch, once no cached launch or build is in flight.
+// into claim slot b = L % kClaimSlots; after the launch the build stream (the context's own stream) builds the slot's
+// payloads, flips them valid, frees the slot (slot_free[b]) and copies the counters for the host, so no launch waits for
+// a build unless kClaimSlots launches in a row are still waiting for theirs. When a launch finds the free list empty,
+// the host learns it from that copy and compacts the cache before a later launch, once no cached launch or build is in
+// flight.
 constexpr int kClaimSlots = 8;
 struct PendingBuild {  // a launch's builds not enqueued yet (launch_shard with defer_build: after the caller's copies)
   bool pending = false;
