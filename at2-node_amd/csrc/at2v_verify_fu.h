@@ -39,6 +39,13 @@ namespace at2v {
 #ifndef AT2V_TABLES_EARLY
 #define AT2V_TABLES_EARLY 0
 #endif
+// AT2V_DECODE_LATE = 1: A and R are decoded after SHA-512, the lattice reduction and the recoding, right before their
+// tables, so only the 24 digit words (not the two decoded points, 80 words) are live across those phases. The verdict is
+// the same conjunction of checks in another order; a lane whose decode fails may set the wave's window count, which only
+// costs windows.
+#ifndef AT2V_DECODE_LATE
+#define AT2V_DECODE_LATE 0
+#endif
 
 // [j]P, j = 0..8, cached form, into tp (one table; the A/B form of the interleaved build)
 template <class TabP>
@@ -72,8 +79,12 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
   }
   // V2: decode A and R; R must be canonical (y < p, not x = 0 with the sign bit)
+#if !AT2V_DECODE_LATE
   gu_p3 A, R;
-#if AT2V_TABLES_EARLY
+#endif
+#if AT2V_DECODE_LATE
+  // (after the reduction, below)
+#elif AT2V_TABLES_EARLY
   // 1: both tables early; 2: A's table early, R kept live (its table after the reduction); 3: R's table early (sign of
   // c1 per digit), A kept live
   if (kCacheable && a_cached) {  // [j]A comes from the cache entry
@@ -102,7 +113,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   ok &= enc_y_canonical(Rw);
   ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
 #endif
-#if AT2V_PARK_POINTS && !AT2V_TABLES_EARLY
+#if AT2V_PARK_POINTS && !AT2V_TABLES_EARLY && !AT2V_DECODE_LATE
   // A and R are not used again until the tables are built (after SHA-512, the lattice reduction and the recoding), and
   // holding their 80 words through those phases is what makes the compiler spill (one scratch reload and wait per
   // word, ~50 of them at the table build). Park them in the lanes' table slots (entry 8, written last by the build)
@@ -150,7 +161,29 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
 
   // tables [j]A and [j](+-R), j = 0..8: one after the other (AT2V_TABLES_X2 = 0, the default since round 3: the pair's
   // extra live registers cost more in spills than its ILP gains, profiles/r03q), or as one interleaved pair
-#if AT2V_TABLES_EARLY
+#if AT2V_DECODE_LATE
+  const int rflip = 0;
+  if (kCacheable && a_cached) {  // [j]A comes from the cache entry
+    ok &= a_cached_ok;
+  } else {
+    gu_p3 A;
+    ok &= gu_frombytes(A, Aw);
+    build_a_table_from(A, ta);
+  }
+  {
+    gu_p3 R;
+    ok &= gu_frombytes(R, Rw);
+    ok &= enc_y_canonical(Rw);
+    ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
+    if (hs.c1_neg) {
+      fu_neg(R.X, R.X, FU_KC);
+      fu_carry(R.X);
+      fu_neg(R.T, R.T, FU_KC);
+      fu_carry(R.T);
+    }
+    build_a_table_from(R, tr);
+  }
+#elif AT2V_TABLES_EARLY
   const int rflip = AT2V_TABLES_EARLY != 2 ? hs.c1_neg : 0;  // [c1]R = [|c1|](-R) when c1 < 0: flips every R digit
   if (AT2V_TABLES_EARLY == 2) {
     if (hs.c1_neg) {
