@@ -110,6 +110,12 @@ struct DevTabA {
     static_assert(sizeof(Cached) == 160, "cached point: 40 words");
     if (kIdentShared && e == 0) return;  // the identity lives in the shared entry
     const int32_t* w = reinterpret_cast<const int32_t*>(&c);
+#if AT2V_EXP_TAB128  // EXPERIMENT (wrong verdicts, timing only): 128-byte entries, one line each (the last 8 words dropped)
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      base[(e - kIdentShared) * 8 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    return;
+#endif
 #pragma unroll
     for (int q = 0; q < 10; ++q)
       base[(e - kIdentShared) * 10 + q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
@@ -152,9 +158,15 @@ struct DevTabA {
   // LDS-DMA (global_load_lds_dwordx4): entry e of every lane -> stage[q][lane], no VGPRs held while the
   // window's four doublings run
   __device__ AT2V_INLINE void prefetch(int e) const {
+#if AT2V_EXP_TAB128
+    const int4* src = (kIdentShared && e == 0) ? ident : base + (e - kIdentShared) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#else
     const int4* src = (kIdentShared && e == 0) ? ident : base + (e - kIdentShared) * 10;
 #pragma unroll
     for (int q = 0; q < 10; ++q)
+#endif
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
                                        (__attribute__((address_space(3))) void*)(stage + q * 64), 16,
                                        0, 0);
