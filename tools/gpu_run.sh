@@ -109,6 +109,9 @@ for st in "$@"; do
     abcomb=*) libs=""
           for v in $(echo "${st#abcomb=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
           run abcomb 900 python3 tools/ab_bench.py $libs --rounds 12 --senders 64 --comb ;;
+    abx=*) libs=""  # experiment builds (wrong verdicts allowed), distinct keys
+          for v in $(echo "${st#abx=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
+          run abx 900 python3 tools/ab_bench.py $libs --rounds 12 --no-check ;;
     abcombx=*) libs=""  # experiment builds (wrong verdicts allowed)
           for v in $(echo "${st#abcombx=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
           run abcombx 900 python3 tools/ab_bench.py $libs --rounds 12 --senders 64 --comb --no-check ;;
