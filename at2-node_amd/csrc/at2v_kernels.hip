@@ -97,8 +97,47 @@ constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
 // across the 10 loads) whatever entry index each lane selects. (r01 interleaved lanes per 16-byte
 // granule: lanes with different digits then touched up to 9 different 1 KiB rows per load,
 // ~9x read amplification — profiles/r01 FETCH_SIZE.)
+// AT2V_TAB_PACK = 1: per-lane table entries packed into 128 B, one cache line per entry instead of two (the table reads
+// of a verify go from ~16.9 to ~8.4 KB). Each coordinate is carried at the table build and its 10 limbs
+// (255 bits, limb 1 given a 26th bit for its carry) packed into 8 words: word k holds limb k (k < 8) in its low
+// kPackW[k] bits, and limbs 8 and 9 (51 bits) fill the words' free high bits. A timing-only build with the entries
+// truncated to one line measured +3.6% (AT2V_EXP_TAB128, profiles/r04zi).
+#ifndef AT2V_TAB_PACK
+#define AT2V_TAB_PACK 0
+#endif
+
+// carried element -> 8 words (see AT2V_TAB_PACK)
+__device__ AT2V_INLINE void fu_pack8(uint32_t o[8], const fu& f) {
+  const uint32_t hl = f.v[8] | (f.v[9] << 26), hh = f.v[9] >> 6;  // H = limb 8 | limb 9 << 26 (51 bits)
+  o[0] = f.v[0] | (hl << 26);
+  o[1] = f.v[1] | ((hl >> 6) << 26);
+  o[2] = f.v[2] | ((hl >> 12) << 26);
+  o[3] = f.v[3] | ((hl >> 18) << 25);
+  o[4] = f.v[4] | ((hl >> 25) << 26);
+  o[5] = f.v[5] | (((hl >> 31) | (hh << 1)) << 25);
+  o[6] = f.v[6] | ((hh >> 6) << 26);
+  o[7] = f.v[7] | ((hh >> 12) << 25);
+}
+__device__ AT2V_INLINE void fu_unpack8(fu& f, const uint32_t i[8]) {
+  const uint32_t m26 = (1u << 26) - 1, m25 = (1u << 25) - 1;
+  f.v[0] = i[0] & m26;
+  f.v[1] = i[1] & m26;
+  f.v[2] = i[2] & m26;
+  f.v[3] = i[3] & m25;
+  f.v[4] = i[4] & m26;
+  f.v[5] = i[5] & m25;
+  f.v[6] = i[6] & m26;
+  f.v[7] = i[7] & m25;
+  const uint32_t p5 = i[5] >> 25;
+  const uint32_t hl = (i[0] >> 26) | ((i[1] >> 26) << 6) | ((i[2] >> 26) << 12) | ((i[3] >> 25) << 18) |
+                      ((i[4] >> 26) << 25) | (p5 << 31);
+  const uint32_t hh = (p5 >> 1) | ((i[6] >> 26) << 6) | ((i[7] >> 25) << 12);
+  f.v[8] = hl & m26;
+  f.v[9] = ((hl >> 26) | (hh << 6)) & m25;
+}
+
 struct DevTabA {
-  int4* base;   // this lane's slot (global): entries kIdentShared..8, 160 B each
+  int4* base;   // this lane's slot (global): entries kIdentShared..8, 160 B each (128 B with AT2V_TAB_PACK)
   int4* stage;  // this wave's 10 x 1 KiB LDS staging buffer for the prefetched entry
   int lane;
   const int4* ident = nullptr;  // the shared identity entry (kIdentShared)
@@ -110,6 +149,24 @@ struct DevTabA {
     static_assert(sizeof(Cached) == 160, "cached point: 40 words");
     if (kIdentShared && e == 0) return;  // the identity lives in the shared entry
     const int32_t* w = reinterpret_cast<const int32_t*>(&c);
+#if AT2V_TAB_PACK
+    {
+      uint32_t pw[32];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        fu x;
+#pragma unroll
+        for (int q = 0; q < 10; ++q) x.v[q] = (uint32_t)w[10 * k + q];
+        fu_carry(x);
+        fu_pack8(pw + 8 * k, x);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        base[(e - kIdentShared) * 8 + q] =
+            make_int4((int)pw[4 * q], (int)pw[4 * q + 1], (int)pw[4 * q + 2], (int)pw[4 * q + 3]);
+      return;
+    }
+#endif
 #if AT2V_EXP_TAB128  // EXPERIMENT (wrong verdicts, timing only): 128-byte entries, one line each (the last 8 words dropped)
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -158,7 +215,7 @@ struct DevTabA {
   // LDS-DMA (global_load_lds_dwordx4): entry e of every lane -> stage[q][lane], no VGPRs held while the
   // window's four doublings run
   __device__ AT2V_INLINE void prefetch(int e) const {
-#if AT2V_EXP_TAB128
+#if AT2V_EXP_TAB128 || AT2V_TAB_PACK
     const int4* src = (kIdentShared && e == 0) ? ident : base + (e - kIdentShared) * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -176,6 +233,23 @@ struct DevTabA {
     static_assert(sizeof(Cached) == 160, "cached point: 40 words");
     AT2V_PROBE(waited, asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
     int32_t* w = reinterpret_cast<int32_t*>(&c);
+#if AT2V_TAB_PACK
+    {
+      uint32_t pw[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int4 v = stage[q * 64 + lane];
+        pw[4 * q] = (uint32_t)v.x;
+        pw[4 * q + 1] = (uint32_t)v.y;
+        pw[4 * q + 2] = (uint32_t)v.z;
+        pw[4 * q + 3] = (uint32_t)v.w;
+      }
+      fu* cf = reinterpret_cast<fu*>(&c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fu_unpack8(cf[k], pw + 8 * k);
+      return;
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < 10; ++q) {
       const int4 v = stage[q * 64 + lane];
@@ -1890,8 +1964,13 @@ hipError_t launch_build_btab(int4* out, hipStream_t stream) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+#if AT2V_TAB_PACK  // the same entry packed (fu_pack8 of 1, 1, 2, 0)
+  static const uint32_t ident[40] = {1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 2, 0, 0, 0,
+                                     0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#else
   static const uint32_t ident[40] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                      2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   const hipError_t e = hipMemcpyAsync(out + (size_t)kNumBtabs * kBtabEntries * 8, ident, sizeof ident,
                                       hipMemcpyHostToDevice, stream);
   if (e != hipSuccess) return e;
