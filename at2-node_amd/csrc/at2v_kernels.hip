@@ -99,11 +99,12 @@ constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
 // ~9x read amplification — profiles/r01 FETCH_SIZE.)
 // AT2V_TAB_PACK = 1: per-lane table entries packed into 128 B, one cache line per entry instead of two (the table reads
 // of a verify go from ~16.9 to ~8.4 KB). Each coordinate is carried at the table build and its 10 limbs
-// (255 bits, limb 1 given a 26th bit for its carry) packed into 8 words: word k holds limb k (k < 8) in its low
-// kPackW[k] bits, and limbs 8 and 9 (51 bits) fill the words' free high bits. A timing-only build with the entries
-// truncated to one line measured +3.6% (AT2V_EXP_TAB128, profiles/r04zi).
+// (255 bits, limb 1 given a 26th bit for its carry) packed into 8 words: word k holds limb k (k < 8) in its low 26 or
+// 25 bits, and limbs 8 and 9 (51 bits) fill the words' free high bits. A timing-only build with the entries truncated
+// to one line measured +3.6% (AT2V_EXP_TAB128, profiles/r04zi); with the carries and the unpacking, +1.0% and +0.1%
+// (medians; minima +0.6%, +0.8%) in two A/B runs, GPU suite 103 passed on it (profiles/r04zk). Default since round 4.
 #ifndef AT2V_TAB_PACK
-#define AT2V_TAB_PACK 0
+#define AT2V_TAB_PACK 1
 #endif
 
 // carried element -> 8 words (see AT2V_TAB_PACK)
