@@ -1,9 +1,10 @@
 """at2v — Python binding (ctypes) of libat2v.so, the MI355X batch Ed25519 verifier.
 
 Thin plumbing over the C ABI in include/at2v.h, used by the tests and bench.py. The product is the
-HIP library. This module has NO CPU fallback: if libat2v.so or a gfx950 device is missing, every
-batch call raises. ``verify_one`` is the per-signature entry point, a CPU function by contract
-(SURVEY §8(b)), not a fallback.
+HIP library. This module has no Python fallback: if libat2v.so is missing, every call raises, and a GPU
+context without a gfx950 device raises. The library's own CPU backend (``BatchVerifier(num_gpus=0)``, and the opt-in
+``cpu_fallback`` of a GPU context) runs the kernels' verify routine compiled for the host over a thread pool; it never
+routes through the oracle. ``verify_one`` is the per-signature entry point, a CPU function by contract.
 
 Reference interface mirrored (drop::crypto::sign, used by at2-node at src/lib.rs:5,19,
 src/client.rs:72-78, src/bin/server/rpc.rs:269,281):
@@ -31,7 +32,7 @@ _POLICIES = {"dalek": POLICY_DALEK_V1, "dalek_v1": POLICY_DALEK_V1, "libsodium":
 # must match include/at2v.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = ("at2v_abi_version", "at2v_create", "at2v_destroy", "at2v_verify_batch", "at2v_verify_batch_device",
                     "at2v_verify_one", "at2v_verify_one_policy", "at2v_strerror", "at2v_gen_records_device",
-                    "at2v_gen_records_senders_device", "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
+                    "at2v_gen_records_senders_device", "at2v_gen_records_keys_device", "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
                     "at2v_comm_get_unique_id", "at2v_comm_init_rank", "at2v_verify_shard_gather_device",
                     "at2v_verify_batch_sharded",
                     "at2v_queue_create", "at2v_queue_destroy", "at2v_queue_submit", "at2v_queue_flush",
@@ -52,14 +53,18 @@ class VerifyError(Exception):
     """Signature rejected (drop::crypto::sign::VerifyError)."""
 
 
-ABI_VERSION = 5  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
+ABI_VERSION = 6  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
 E_PEER = -7      # AT2V_E_PEER: another rank of the communicator failed this collective batch
 
 
 class _Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int),
                 ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32),
-                ("sender_comb", ctypes.c_uint32)]
+                ("sender_comb", ctypes.c_uint32), ("cpu_threads", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+CTX_CPU_FALLBACK = 1   # include/at2v.h AT2V_CTX_CPU_FALLBACK: a failed GPU batch (host buffers) re-runs on the CPU backend
+CTX_ADMIT_FIRST = 2    # include/at2v.h AT2V_CTX_ADMIT_FIRST: sender-cache keys claim a payload at their first sighting
 
 
 SMALL_BATCH_DEFAULT = 32768     # include/at2v.h AT2V_SMALL_BATCH_DEFAULT
@@ -73,7 +78,10 @@ class _Info(ctypes.Structure):
                 ("cache_entries", ctypes.c_uint64), ("cache_chunks", ctypes.c_uint64),
                 ("cache_chunk_hits", ctypes.c_uint64), ("cache_capacity", ctypes.c_uint64),
                 ("cache_claims", ctypes.c_uint64), ("cache_evicted", ctypes.c_uint64),
-                ("cache_compactions", ctypes.c_uint64)]
+                ("cache_compactions", ctypes.c_uint64), ("cpu_threads", ctypes.c_uint64),
+                ("cpu_batches", ctypes.c_uint64), ("cpu_fallbacks", ctypes.c_uint64),
+                ("cache_sightings", ctypes.c_uint64), ("cache_built", ctypes.c_uint64),
+                ("cache_build_us", ctypes.c_uint64)]
 
 
 UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)
@@ -131,6 +139,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.at2v_gen_records_senders_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
                                                     ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P]
     lib.at2v_gen_records_senders_device.restype = ctypes.c_int
+    lib.at2v_gen_records_keys_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
+                                                 ctypes.c_uint32, P, P, P, P, P, P]
+    lib.at2v_gen_records_keys_device.restype = ctypes.c_int
     lib.at2v_sign_batch.argtypes = [P, P, P, P, ctypes.c_size_t, P, P]
     lib.at2v_sign_batch.restype = ctypes.c_int
     lib.at2v_get_info.argtypes = [P, ctypes.POINTER(_Info)]
@@ -199,19 +210,25 @@ def launch_streams(count: int = 2, device: Optional[int] = None) -> list:
 
 
 class BatchVerifier:
-    """Owns an at2v context (one or more gfx950 devices)."""
+    """Owns an at2v context: one or more gfx950 devices, or (num_gpus=0) the library's CPU batch backend."""
 
     def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek", small_batch_max: int = 0,
-                 sender_cache: int = 0, sender_comb: bool = False):
+                 sender_cache: int = 0, sender_comb: bool = False, cpu_threads: int = 0, cpu_fallback: bool = False,
+                 admit_first: bool = False):
         """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
         0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel.
         sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off).
         sender_comb: with sender_cache, also keep a comb of -A per cached key (1.7 MB of HBM each, plus one 67 MB comb
         of B per context; include/at2v.h): chunks whose senders are all cached verify by table additions only
-        (at2v_comb.h), launches of every size."""
+        (at2v_comb.h), launches of every size.
+        num_gpus=0: the CPU batch backend (no device; cpu_threads host threads, 0 = every usable CPU).
+        cpu_fallback: a GPU context re-runs a host-buffer batch on the CPU backend after a device error (same verdicts;
+        info()["cpu_fallbacks"] counts it). admit_first: cache keys claim a payload at their first sighting."""
         self._lib = load_library()
         self.policy = _POLICIES[policy]
-        opts = _Opts(device, num_gpus, self.policy, small_batch_max, sender_cache, 1 if sender_comb else 0)
+        flags = (CTX_CPU_FALLBACK if cpu_fallback else 0) | (CTX_ADMIT_FIRST if admit_first else 0)
+        opts = _Opts(device, num_gpus, self.policy, small_batch_max, sender_cache, 1 if sender_comb else 0,
+                     cpu_threads, flags)
         h = ctypes.c_void_p()
         _check(self._lib.at2v_create(ctypes.byref(opts), ctypes.byref(h)), "at2v_create")
         self._h = h
@@ -300,6 +317,12 @@ class BatchVerifier:
             return
         _check(self._lib.at2v_gen_records_device(self._h, cfg_seed, first, n, msg_len, d_pk, d_sig, d_msg,
                                                  d_off or None, stream or None), "at2v_gen_records_device")
+
+    def gen_records_keys_device(self, cfg_seed: int, first: int, n: int, msg_len: int, d_keys: int, d_pk: int,
+                                d_sig: int, d_msg: int, d_off: Optional[int], stream: int = 0) -> None:
+        """GPU generator with a key per record: record i signed by seed index d_keys[i] (u64 device array)"""
+        _check(self._lib.at2v_gen_records_keys_device(self._h, cfg_seed, first, n, msg_len, d_keys, d_pk, d_sig, d_msg,
+                                                      d_off or None, stream or None), "at2v_gen_records_keys_device")
 
     def decode_points(self, pts: np.ndarray) -> np.ndarray:
         """bool[n]: 32-byte encodings that decode under dalek rules (GPU kernel)"""

@@ -66,18 +66,20 @@ class AccountError(Exception):
 
 QUEUE_EAGER = 1  # include/at2v.h AT2V_QUEUE_EAGER: also seal whenever no batch is in flight
 QUEUE_SENDER_COMB = 2  # include/at2v.h AT2V_QUEUE_SENDER_COMB: per-sender combs in the queue's context
+QUEUE_CPU = 4  # include/at2v.h AT2V_QUEUE_CPU: batches verified by the CPU backend (no device)
+QUEUE_CPU_FALLBACK = 8  # include/at2v.h AT2V_QUEUE_CPU_FALLBACK: a batch that fails on the device re-runs on the CPU
 
 
 class _QueueOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("policy", ctypes.c_int), ("max_batch", ctypes.c_uint32),
                 ("max_delay_us", ctypes.c_uint32), ("max_msg_bytes", ctypes.c_uint32), ("depth", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32), ("cpu_threads", ctypes.c_uint32)]
 
 
 class _QueueStats(ctypes.Structure):
     _fields_ = [("submitted", ctypes.c_uint64), ("completed", ctypes.c_uint64), ("batches", ctypes.c_uint64),
                 ("failed_batches", ctypes.c_uint64), ("mean_batch", ctypes.c_double), ("p50_us", ctypes.c_double),
-                ("p99_us", ctypes.c_double), ("max_us", ctypes.c_double)]
+                ("p99_us", ctypes.c_double), ("max_us", ctypes.c_double), ("cpu_fallbacks", ctypes.c_uint64)]
 
 
 class _SendAsset(ctypes.Structure):
@@ -143,13 +145,16 @@ class IngestQueue:
 
     def __init__(self, device: int = 0, policy="dalek", max_batch: int = 65536, max_delay_us: int = 1000,
                  max_msg_bytes: int = 256, depth: int = 3, eager: bool = False, sender_comb: bool = False,
-                 sender_cache: int = 0):
+                 sender_cache: int = 0, cpu: bool = False, cpu_fallback: bool = False, cpu_threads: int = 0):
         """eager: also seal whenever no batch is in flight (latency mode); sender_comb: per-sender combs in the queue's
-        context (at2v_comb.h) for `sender_cache` keys (0 = 1024; 1.7 MB of HBM per key)"""
+        context (at2v_comb.h) for `sender_cache` keys (0 = 1024; 1.7 MB of HBM per key); cpu: verify on the library's
+        CPU backend (no device); cpu_fallback: a batch that fails on the device is verified on the CPU backend instead"""
         from . import _POLICIES
         self._lib = _lib()
-        o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth,
-                       (QUEUE_EAGER if eager else 0) | (QUEUE_SENDER_COMB if sender_comb else 0), sender_cache)
+        flags = ((QUEUE_EAGER if eager else 0) | (QUEUE_SENDER_COMB if sender_comb else 0) | (QUEUE_CPU if cpu else 0)
+                 | (QUEUE_CPU_FALLBACK if cpu_fallback else 0))
+        o = _QueueOpts(device, _POLICIES[policy], max_batch, max_delay_us, max_msg_bytes, depth, flags, sender_cache,
+                       cpu_threads)
         h = ctypes.c_void_p()
         _chk(self._lib.at2v_queue_create(ctypes.byref(o), ctypes.byref(h)), "at2v_queue_create")
         self._h = h

@@ -29,6 +29,7 @@
 
 #include "../../include/at2v.h"
 #include "at2v_cache.h"
+#include "at2v_cpu.h"
 #include "at2v_shard.h"
 
 namespace at2v {
@@ -37,8 +38,8 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
                          const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache);
 size_t btab_bytes();
 hipError_t launch_build_btab(int4* out, hipStream_t stream);
-hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders, uint8_t* pk,
-                      uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream);
+hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders,
+                      const uint64_t* keys, uint8_t* pk, uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream);
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* msg, uint32_t msg_total, const uint32_t* off, uint32_t n,
                        uint8_t* pk, uint8_t* sig, hipStream_t stream);
 hipError_t launch_decode(const uint8_t* pts, uint32_t n, uint32_t* out, hipStream_t stream);
@@ -74,8 +75,8 @@ struct DevBuf {
 // into claim slot b = L % kClaimSlots; after the launch the build stream (the context's own stream) builds the slot's
 // payloads, flips them valid, frees the slot (slot_free[b]) and copies the counters for the host, so no launch waits for
 // a build unless kClaimSlots launches in a row are still waiting for theirs. When a launch finds the free list empty,
-// the host learns it from that copy and compacts the cache before a later launch, once no cached launch or build is in
-// flight.
+// the host learns it from that copy and enqueues a compaction on the build stream (cache_before_launch); no launch waits
+// for it.
 constexpr int kClaimSlots = 8;
 struct PendingBuild {  // a launch's builds not enqueued yet (launch_shard with defer_build: after the caller's copies)
   bool pending = false;
@@ -87,7 +88,7 @@ struct SenderCache {
   at2v::CacheArgs args{};
   DevBuf tags[2], entries[2];  // the live tag table / entries ([cur]) and the compaction target ([cur ^ 1])
   int cur = 0;
-  DevBuf payload, free_slots, used, ctl, bcomb, claim_list[kClaimSlots];
+  DevBuf payload, free_slots, used, ctl, bcomb, seen, claim_list[kClaimSlots];
   // Builds run on the context's own stream (the shard's), which a caller's launches on its own streams never use: a
   // separate build stream would share one of the process's 4 hardware queues (GPU_MAX_HW_QUEUES, round robin) with a
   // caller's stream, whose next copy or launch then waited behind a 0.8 ms comb build (config 5 p99).
@@ -96,10 +97,16 @@ struct SenderCache {
   hipEvent_t claims_ready[kClaimSlots] = {};  // launch stream, after the launch that filled slot b
   hipEvent_t slot_free[kClaimSlots] = {};     // build stream, after slot b's flip
   hipEvent_t built = nullptr;                 // build stream, after the last flip
+  // recorded after the last compaction (build stream). Until it has completed, launches read the old table and claim
+  // nothing; the first launch after it swaps the tables. So no launch probes a tag table that is still being filled or
+  // pops the free list while it is being rebuilt, whatever stream it runs on (in round 4 a launch on the other
+  // scratch set's stream could overlap a compaction enqueued on its neighbour's stream).
+  hipEvent_t compacted = nullptr;
   unsigned long long* host_ctl = nullptr;  // pinned copy of the device counters, refreshed after every cached launch
   hipEvent_t ctl_copied = nullptr;
   bool copy_pending = false;
-  bool compact_pending = false;
+  bool compact_pending = false;  // a launch found the cache full: compact before a later launch
+  bool compacting = false;       // a compaction is enqueued on the build stream and has not been swapped in yet
   uint64_t launches = 0;  // launch epochs (entries record the last launch that used them)
 };
 
@@ -130,7 +137,11 @@ constexpr size_t kGatherWindow = 65536;
 struct at2v_ctx {
   at2v_policy policy = AT2V_POLICY_DALEK_V1;
   uint32_t pair_max = AT2V_SMALL_BATCH_DEFAULT;  // launches of <= this many records: low-latency kernel
-  std::vector<Shard> shards;
+  uint32_t flags = 0;         // at2v_opts.flags (AT2V_CTX_*)
+  std::vector<Shard> shards;  // empty: a CPU-backend context (at2v_opts.num_gpus = 0)
+  at2v::CpuPool* cpu = nullptr;  // the CPU backend (a CPU context, or AT2V_CTX_CPU_FALLBACK)
+  uint64_t cpu_batches = 0, cpu_fallbacks = 0;
+  uint32_t test_fail_launches = 0;  // AT2V_TEST_FAIL_LAUNCH (tests only): that many launches fail before the kernel
   ncclComm_t comm = nullptr;  // at2v_comm_init_rank (one rank per process, the context's first device)
   int rank = 0, world = 1;
   DevBuf window;              // at2v_verify_batch_sharded: world x kGatherWindow words, one all-gather round
@@ -187,10 +198,11 @@ void free_cache(SenderCache*& c) {
   if (!c) return;
   if (c->build) (void)hipStreamSynchronize(c->build);  // (the shard's stream: destroyed with the shard)
   for (DevBuf* b : {&c->tags[0], &c->tags[1], &c->entries[0], &c->entries[1], &c->payload, &c->free_slots, &c->used,
-                    &c->ctl, &c->bcomb})
+                    &c->ctl, &c->bcomb, &c->seen})
     b->release();
   for (DevBuf& b : c->claim_list) b.release();
   if (c->built) (void)hipEventDestroy(c->built);
+  if (c->compacted) (void)hipEventDestroy(c->compacted);
   if (c->host_ctl) (void)hipHostFree(c->host_ctl);
   if (c->ctl_copied) (void)hipEventDestroy(c->ctl_copied);
   for (int j = 0; j < kClaimSlots; ++j) {
@@ -204,7 +216,7 @@ void free_cache(SenderCache*& c) {
 // Per-sender cache for `capacity` distinct keys on the current device: 2x as many tag slots (open addressing at
 // load <= 1/2), one payload per key. AT2V_TEST_CACHE_FP_BITS (tests only) keeps that many fingerprint bits, so distinct
 // keys collide and the byte comparison in the verify kernels is exercised.
-int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
+int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit_first) {
   SenderCache* c = new (std::nothrow) SenderCache;
   if (!c) return AT2V_E_OOM;
   s.cache = c;
@@ -217,6 +229,9 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
   a.seed = seed;
   a.fp_mask = ~0ull;
   a.comb = comb ? 1 : 0;
+  a.admit_first = admit_first ? 1 : 0;
+  // the sighting filter: 2^21 fingerprints (16 MB), so a key seen twice within ~a million records is still found
+  a.seen_mask = (1u << 21) - 1;
   if (const char* b = std::getenv("AT2V_TEST_CACHE_FP_BITS")) {
     const int bits = std::atoi(b);
     if (bits > 0 && bits < 64) a.fp_mask = (1ull << bits) - 1ull;
@@ -233,12 +248,15 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
   AT2V_TRY(c->used.ensure((size_t)capacity * 4));
   AT2V_TRY(c->ctl.ensure(ctl_bytes));
   AT2V_TRY(hipMemset(c->ctl.p, 0, c->ctl.cap));
+  AT2V_TRY(c->seen.ensure(((size_t)a.seen_mask + 1) * 8));
+  AT2V_TRY(hipMemset(c->seen.p, 0, c->seen.cap));
   for (int j = 0; j < kClaimSlots; ++j) AT2V_TRY(c->claim_list[j].ensure((size_t)capacity * 16));
   a.tags = (unsigned long long*)c->tags[0].p;
   a.entries = (int4*)c->entries[0].p;
   a.payload = (int4*)c->payload.p;
   a.free_slots = (uint32_t*)c->free_slots.p;
   a.ctl = (unsigned long long*)c->ctl.p;
+  a.seen = (unsigned long long*)c->seen.p;
   a.new_list = (uint4*)c->claim_list[0].p;
   if (comb) {  // the comb of B, built once
     AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes()));
@@ -259,30 +277,51 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb) {
   }
   AT2V_TRY(hipEventCreateWithFlags(&c->built, hipEventDisableTiming));
   AT2V_TRY(hipEventRecord(c->built, c->build));
+  AT2V_TRY(hipEventCreateWithFlags(&c->compacted, hipEventDisableTiming));
+  AT2V_TRY(hipEventRecord(c->compacted, c->build));
   return AT2V_OK;
 }
 
 // Before a cached launch on `stream`: wait until the launch's claim slot is free; if an earlier launch found the cache
-// full (its counters' copy has landed), compact it first, once every cached launch and build is done.
-hipError_t cache_before_launch(SenderCache& c, hipStream_t stream, int j) {
+// full (its counters' copy has landed), enqueue a compaction on the build stream, behind every launch and build issued
+// so far. Launches issued while it runs look keys up in the old table and claim nothing (CacheArgs::no_claim), so they
+// neither wait for it nor touch what it rebuilds (the free list, the spare table). The first launch after it has
+// completed swaps the tables in; from then on the build stream also waits for every launch issued before the swap, so a
+// payload an evicted entry still held (maybe read by a lookup-only launch) is rebuilt for another key only once those
+// launches are done.
+hipError_t cache_before_launch(SenderCache& c, Shard& s, hipStream_t stream, int j) {
   hipError_t e = hipStreamWaitEvent(stream, c.slot_free[j], 0);
   if (e == hipSuccess && c.copy_pending && hipEventQuery(c.ctl_copied) == hipSuccess) {
     c.copy_pending = false;
     if (c.host_ctl[at2v::kCtlFull]) c.compact_pending = true;
   }
-  if (e == hipSuccess && c.compact_pending) {
-    for (int k = 0; k < kClaimSlots && e == hipSuccess; ++k) e = hipStreamWaitEvent(stream, c.claims_ready[k], 0);
-    if (e == hipSuccess) e = hipStreamWaitEvent(stream, c.built, 0);
+  auto wait_all_launches = [&](hipStream_t st) {  // every launch so far: the last one on each scratch set
+    hipError_t r = hipSuccess;
+    for (int k = 0; k < s.sets && r == hipSuccess; ++k) r = hipStreamWaitEvent(st, s.scratch_free[k], 0);
+    return r;
+  };
+  if (e == hipSuccess && c.compacting && hipEventQuery(c.compacted) == hipSuccess) {
+    e = wait_all_launches(c.build);
+    if (e == hipSuccess) {
+      const int nx = c.cur ^ 1;
+      c.cur = nx;
+      c.args.tags = (unsigned long long*)c.tags[nx].p;
+      c.args.entries = (int4*)c.entries[nx].p;
+      c.compacting = false;
+    }
+  }
+  if (e == hipSuccess && c.compact_pending && !c.compacting) {
+    e = wait_all_launches(c.build);  // (the builds before it are on the build stream already)
     const int nx = c.cur ^ 1;
     at2v::CacheCompactArgs x{(unsigned long long*)c.tags[nx].p, (int4*)c.entries[nx].p, (uint32_t*)c.used.p};
-    if (e == hipSuccess) e = at2v::launch_cache_compact(c.args, x, stream);
+    if (e == hipSuccess) e = at2v::launch_cache_compact(c.args, x, c.build);
+    if (e == hipSuccess) e = hipEventRecord(c.compacted, c.build);
     if (e == hipSuccess) {
-      c.cur = nx;
-      c.args.tags = x.new_tags;
-      c.args.entries = x.new_entries;
+      c.compacting = true;
       c.compact_pending = false;
     }
   }
+  c.args.no_claim = c.compacting ? 1 : 0;
   return e;
 }
 
@@ -294,9 +333,14 @@ hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
   if (e == hipSuccess) e = at2v::launch_cache_build(b.args, b.max_claims, c.build);
   if (e == hipSuccess) e = hipEventRecord(c.slot_free[b.slot], c.build);
   if (e == hipSuccess) e = hipEventRecord(c.built, c.build);
-  if (e == hipSuccess) e = hipMemcpyAsync(c.host_ctl, c.ctl.p, c.ctl.cap, hipMemcpyDeviceToHost, c.build);
-  if (e == hipSuccess) e = hipEventRecord(c.ctl_copied, c.build);
-  c.copy_pending = e == hipSuccess;
+  // A new copy only once the host has seen the previous one: re-recording the event behind every launch's builds would
+  // keep it "not ready" for as long as launches arrive faster than the build stream drains, and the host would never
+  // learn that the cache is full (compaction starved; the counters it reads may be a few launches old instead).
+  if (e == hipSuccess && !c.copy_pending) {
+    e = hipMemcpyAsync(c.host_ctl, c.ctl.p, c.ctl.cap, hipMemcpyDeviceToHost, c.build);
+    if (e == hipSuccess) e = hipEventRecord(c.ctl_copied, c.build);
+    c.copy_pending = e == hipSuccess;
+  }
   return e;
 }
 
@@ -310,11 +354,16 @@ hipError_t flush_cache_build(Shard& s) {
 
 // One verify launch on shard s (current device = s.device), on `stream`. The launch takes the shard's next scratch set
 // and waits for the launch that last used that set, on whatever stream that ran; launches on different streams may
-// therefore run concurrently (on one stream they are ordered anyway). Cached launches also wait for the previous cached
-// launch (the cache's tags and per-launch slot arrays are shared). The verdict words are zeroed first (fail closed).
+// therefore run concurrently (on one stream they are ordered anyway). Cached launches may overlap too: they share the tag
+// table through atomics, each has its own claim slot (and waits for that slot's previous builds), and every cached launch
+// after a compaction waits for it (cache_before_launch). The verdict words are zeroed first (fail closed).
 hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                         uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream,
                         bool zero_verdicts = true, bool defer_build = false) {
+  if (ctx->test_fail_launches) {  // test hook: a launch failure, as a faulting device would report it
+    --ctx->test_fail_launches;
+    return hipErrorLaunchFailure;
+  }
   const int j = (int)(s.next_set++ % (unsigned)s.sets);
   hipError_t e = hipStreamWaitEvent(stream, s.scratch_free[j], 0);
   // the cache serves the throughput kernel (launches above small_batch_max records; with combs, every launch)
@@ -324,7 +373,7 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   if (c && c->args.comb && n <= ctx->pair_max) zero_verdicts = false;
   if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
   const int cs = c ? (int)(c->launches % kClaimSlots) : 0;
-  if (e == hipSuccess && c) e = cache_before_launch(*c, stream, cs);
+  if (e == hipSuccess && c) e = cache_before_launch(*c, s, stream, cs);
   at2v::CacheArgs ca{};
   if (c) {
     c->args.count_word = at2v::kCtlClaims0 + cs;
@@ -398,16 +447,35 @@ extern "C" {
 int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
-  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1, 0, 0, 0};
+  at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0};
   if (opts) o = *opts;
-  if (o.num_gpus <= 0) o.num_gpus = 1;
+  if (o.num_gpus < 0 || o.num_gpus > 64) return AT2V_E_INVALID;
   if (o.policy != AT2V_POLICY_DALEK_V1 && o.policy != AT2V_POLICY_LIBSODIUM_1_0_18) return AT2V_E_INVALID;
+  if (o.flags & ~(AT2V_CTX_CPU_FALLBACK | AT2V_CTX_ADMIT_FIRST)) return AT2V_E_INVALID;
+  if (o.num_gpus == 0) {  // the CPU batch backend: no HIP call at all
+    at2v_ctx* c = new (std::nothrow) at2v_ctx;
+    if (!c) return AT2V_E_OOM;
+    c->policy = o.policy;
+    c->flags = o.flags;
+    c->cpu = at2v::cpu_pool_create(o.cpu_threads);
+    if (!c->cpu) {
+      delete c;
+      return AT2V_E_OOM;
+    }
+    *out = c;
+    return AT2V_OK;
+  }
+  // AT2V_TEST_DEVICE_ALIAS (tests only): shard g runs on device (device + g) % ndev, so a one-GPU box executes the
+  // single-process multi-device path (split, per-shard streams, scratch, B tables and caches) with num_gpus > ndev
+  const bool alias = std::getenv("AT2V_TEST_DEVICE_ALIAS") && std::atoi(std::getenv("AT2V_TEST_DEVICE_ALIAS")) != 0;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return AT2V_E_NODEVICE;
-  if (o.device < 0 || o.device + o.num_gpus > ndev) return AT2V_E_NODEVICE;
+  if (o.device < 0 || o.device >= ndev || (!alias && o.device + o.num_gpus > ndev)) return AT2V_E_NODEVICE;
   at2v_ctx* c = new (std::nothrow) at2v_ctx;
   if (!c) return AT2V_E_OOM;
   c->policy = o.policy;
+  c->flags = o.flags;
+  if (const char* v = std::getenv("AT2V_TEST_FAIL_LAUNCH")) c->test_fail_launches = (uint32_t)std::strtoul(v, nullptr, 10);
   c->pair_max = o.small_batch_max == 0 ? AT2V_SMALL_BATCH_DEFAULT
                 : o.small_batch_max == AT2V_SMALL_BATCH_OFF ? 0u : o.small_batch_max;
   c->shards.resize((size_t)o.num_gpus);
@@ -415,12 +483,17 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   (void)hipGetDevice(&prev);
   std::random_device rd;
   for (int g = 0; g < o.num_gpus; ++g) {
-    int rc = init_shard(c->shards[(size_t)g], o.device + g);
+    int rc = init_shard(c->shards[(size_t)g], alias ? (o.device + g) % ndev : o.device + g);
     if (rc == AT2V_OK && o.sender_cache)
-      rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd(), o.sender_comb != 0);
+      rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd(), o.sender_comb != 0,
+                      (o.flags & AT2V_CTX_ADMIT_FIRST) != 0);
     // the cross-rank failure flag of at2v_comm_init_rank / at2v_verify_batch_sharded (first device): allocated here,
     // so a rank whose communicator set-up fails can still join the outcome all-reduce
     if (rc == AT2V_OK && g == 0) rc = hip_code(c->status.ensure(4));
+    if (rc == AT2V_OK && g == 0 && (o.flags & AT2V_CTX_CPU_FALLBACK)) {
+      c->cpu = at2v::cpu_pool_create(o.cpu_threads);
+      if (!c->cpu) rc = AT2V_E_OOM;
+    }
     if (rc != AT2V_OK) {
       (void)hipSetDevice(prev);
       at2v_destroy(c);
@@ -469,6 +542,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     s.verdict.release();
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+  at2v::cpu_pool_destroy(ctx->cpu);
   delete ctx;
 }
 
@@ -479,6 +553,11 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
   if (!pk || !sig || !msg_off || !verdicts || n >= (1u << 31)) return AT2V_E_INVALID;
   if (!msg && msg_off[n] != msg_off[0]) return AT2V_E_INVALID;
   if (!at2v::offsets_valid(msg_off, n)) return AT2V_E_INVALID;  // whole batch, before any device work
+  if (ctx->shards.empty()) {  // CPU context
+    at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
+    ++ctx->cpu_batches;
+    return AT2V_OK;
+  }
   int prev = 0;
   (void)hipGetDevice(&prev);
   const size_t G = ctx->shards.size();
@@ -523,6 +602,16 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     hipError_t e = hipEventSynchronize(s.copied);
     if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
+  if (rc != AT2V_OK && ctx->cpu) {
+    // AT2V_CTX_CPU_FALLBACK: the records are still in the caller's host buffers. Drain what the shards enqueued (no
+    // verdict copy of this call may land after the CPU's words), then verify the whole batch on the CPU backend.
+    for (Shard& s : ctx->shards)
+      if (hipSetDevice(s.device) == hipSuccess) (void)hipStreamSynchronize(s.stream);
+    at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
+    ++ctx->cpu_batches;
+    ++ctx->cpu_fallbacks;
+    rc = AT2V_OK;
+  }
   (void)hipSetDevice(prev);
   return rc;
 }
@@ -534,6 +623,7 @@ int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* 
   if (n == 0) return AT2V_OK;
   if (!d_pk || !d_sig || !d_msg_off || !d_verdicts || n >= (1u << 31) || msg_bytes >= (1ull << 32))
     return AT2V_E_INVALID;
+  if (ctx->shards.empty()) return AT2V_E_NODEVICE;
   if (!aligned(d_pk, 16) || !aligned(d_sig, 16) || !aligned(d_msg_off, 4) || !aligned(d_verdicts, 4))
     return AT2V_E_ALIGN;
   Shard& s = ctx->shards[0];
@@ -560,6 +650,7 @@ int at2v_comm_get_unique_id(uint8_t out[AT2V_UNIQUE_ID_BYTES]) {
 }
 
 int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BYTES], int rank, int world) {
+  if (ctx && ctx->shards.empty()) return AT2V_E_NODEVICE;
   if (!ctx || !unique_id || world < 1 || rank < 0 || rank >= world || ctx->comm || ctx->shards.size() != 1)
     return AT2V_E_INVALID;
   ncclUniqueId id;
@@ -708,7 +799,7 @@ const char* at2v_strerror(int code) {
   switch (code) {
     case AT2V_OK: return "ok";
     case AT2V_E_INVALID: return "invalid argument";
-    case AT2V_E_NODEVICE: return "no usable gfx950 device";
+    case AT2V_E_NODEVICE: return "no usable gfx950 device (or a device entry point on a CPU context)";
     case AT2V_E_HIP: return "HIP runtime error";
     case AT2V_E_OOM: return "out of memory";
     case AT2V_E_ALIGN: return "misaligned device pointer";
@@ -724,23 +815,38 @@ int at2v_gen_records_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, si
                                          hip_stream);
 }
 
-int at2v_gen_records_senders_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
-                                    uint64_t senders, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
-                                    uint32_t* d_msg_off, void* hip_stream) {
+static int gen_records(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len, uint64_t senders,
+                       const uint64_t* d_keys, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg, uint32_t* d_msg_off,
+                       void* hip_stream) {
   if (!ctx) return AT2V_E_INVALID;
   if (n == 0) return AT2V_OK;
   if (!d_pk || !d_sig || (!d_msg && msg_len) || n >= (1u << 31) || (uint64_t)n * msg_len >= (1ull << 32))
     return AT2V_E_INVALID;
-  if (!aligned(d_pk, 4) || !aligned(d_sig, 4) || (d_msg_off && !aligned(d_msg_off, 4))) return AT2V_E_ALIGN;
+  if (ctx->shards.empty()) return AT2V_E_NODEVICE;
+  if (!aligned(d_pk, 4) || !aligned(d_sig, 4) || (d_msg_off && !aligned(d_msg_off, 4)) || !aligned(d_keys, 8))
+    return AT2V_E_ALIGN;
   Shard& s = ctx->shards[0];
   int prev = 0;
   (void)hipGetDevice(&prev);
   hipError_t e = hipSetDevice(s.device);
   if (e == hipSuccess)
-    e = at2v::launch_gen(cfg_seed, first, (uint32_t)n, msg_len, senders, d_pk, d_sig, d_msg, d_msg_off,
+    e = at2v::launch_gen(cfg_seed, first, (uint32_t)n, msg_len, senders, d_keys, d_pk, d_sig, d_msg, d_msg_off,
                          (hipStream_t)hip_stream);
   (void)hipSetDevice(prev);
   return hip_code(e);
+}
+
+int at2v_gen_records_senders_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
+                                    uint64_t senders, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
+                                    uint32_t* d_msg_off, void* hip_stream) {
+  return gen_records(ctx, cfg_seed, first, n, msg_len, senders, nullptr, d_pk, d_sig, d_msg, d_msg_off, hip_stream);
+}
+
+int at2v_gen_records_keys_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
+                                 const uint64_t* d_keys, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
+                                 uint32_t* d_msg_off, void* hip_stream) {
+  if (n && !d_keys) return AT2V_E_INVALID;
+  return gen_records(ctx, cfg_seed, first, n, msg_len, 0, d_keys, d_pk, d_sig, d_msg, d_msg_off, hip_stream);
 }
 
 int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, const uint32_t* msg_off, size_t n,
@@ -748,6 +854,7 @@ int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, con
   if (!ctx) return AT2V_E_INVALID;
   if (n == 0) return AT2V_OK;
   if (!seeds || !msg_off || !pk_out || !sig_out || n >= (1u << 31)) return AT2V_E_INVALID;
+  if (ctx->shards.empty()) return AT2V_E_NODEVICE;  // (signing is the client's side, not the verify path)
   Shard& s = ctx->shards[0];
   const uint32_t mb0 = msg_off[0], mb1 = msg_off[n];
   if (mb1 < mb0 || (!msg && mb1 != mb0)) return AT2V_E_INVALID;
@@ -788,6 +895,10 @@ int at2v_decode_points(at2v_ctx* ctx, const uint8_t* pts, size_t n, uint32_t* va
   if (!ctx) return AT2V_E_INVALID;
   if (n == 0) return AT2V_OK;
   if (!pts || !valid_words || n >= (1u << 31)) return AT2V_E_INVALID;
+  if (ctx->shards.empty()) {  // CPU context: the kernels' decode routine on the host
+    at2v::cpu_decode_points(ctx->cpu, pts, n, valid_words);
+    return AT2V_OK;
+  }
   Shard& s = ctx->shards[0];
   int prev = 0;
   (void)hipGetDevice(&prev);
@@ -804,7 +915,12 @@ int at2v_decode_points(at2v_ctx* ctx, const uint8_t* pts, size_t n, uint32_t* va
 }
 
 int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
-  if (!ctx || !out || ctx->shards.empty()) return AT2V_E_INVALID;
+  if (!ctx || !out) return AT2V_E_INVALID;
+  std::memset(out, 0, sizeof *out);
+  out->cpu_threads = at2v::cpu_pool_threads(ctx->cpu);
+  out->cpu_batches = ctx->cpu_batches;
+  out->cpu_fallbacks = ctx->cpu_fallbacks;
+  if (ctx->shards.empty()) return AT2V_OK;  // CPU context: no device geometry
   const Shard& s = ctx->shards[0];
   out->num_gpus = (int)ctx->shards.size();
   out->grid_blocks = s.grid;
@@ -815,8 +931,6 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
   out->rank = ctx->rank;
   out->world = ctx->comm ? ctx->world : 0;
   out->gathers = ctx->gathers;
-  out->cache_entries = out->cache_chunks = out->cache_chunk_hits = 0;
-  out->cache_capacity = out->cache_claims = out->cache_evicted = out->cache_compactions = 0;
   for (const Shard& sh : ctx->shards) {
     // sender-cache counters, summed over devices. Waits for the context's cache work only (its build stream, which
     // follows every cached launch): builds of earlier launches are done and their keys usable when this returns.
@@ -834,6 +948,11 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
       out->cache_claims += w[at2v::kCtlClaimed];
       out->cache_evicted += w[at2v::kCtlEvicted];
       out->cache_compactions += w[at2v::kCtlCompactions];
+      out->cache_sightings += w[at2v::kCtlSighted];
+      out->cache_built += w[at2v::kCtlBuilt];
+      int khz = 0;  // device wall clock (wall_clock64) in kHz
+      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, sh.device) == hipSuccess && khz > 0)
+        out->cache_build_us += w[at2v::kCtlBuildTicks] * 1000ull / (uint64_t)khz;
       out->cache_capacity += cap;
     }
     (void)hipSetDevice(prev);

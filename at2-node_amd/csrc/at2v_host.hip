@@ -7,6 +7,7 @@
 //   * at2v_ledger_*  accounts / recent transactions / apply loop (at2v_ledger.h).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -28,12 +29,36 @@ struct DevSlot {
   size_t msg_at = 0;       // byte offset of msg in both allocations
   void *pk = nullptr, *sig = nullptr, *msg = nullptr, *off = nullptr, *ver = nullptr;
   hipEvent_t uploaded = nullptr, verified = nullptr, done = nullptr;
+  hipStream_t stream = nullptr;  // the compute stream of the slot's last launch
+  bool cpu_done = false;         // the slot's batch was verified on the CPU backend (AT2V_QUEUE_CPU[_FALLBACK])
 };
 constexpr size_t kSingleCopyMax = 2u << 20;
+
+// Sets the queue's device for a scope and restores the caller's current device on every return path: with launches from
+// the producer's thread (at2v_queue_submit in latency mode) a user thread must not find its HIP device switched
+// (ADVICE r4).
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err;
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = prev == device ? hipSuccess : hipSetDevice(device);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
 
 struct HipBackend {
   at2v_ctx* ctx = nullptr;
   int device = 0;
+  // AT2V_QUEUE_CPU: ctx is a CPU context (num_gpus = 0) and every batch is verified on it, synchronously in launch().
+  // AT2V_QUEUE_CPU_FALLBACK: cpu_ctx is a CPU context beside the GPU one; a batch whose launch or completion fails on the
+  // device is verified there from the slot's host records (the verdict words are the slot's pinned host words).
+  bool cpu_only = false;
+  at2v_ctx* cpu_ctx = nullptr;
+  std::atomic<uint64_t> fallbacks{0};
   // three streams of the queue + the context's own (which runs the sender-cache builds): four, one hardware queue each
   // (GPU_MAX_HW_QUEUES = 4), so no verify or copy of the latency path waits behind a comb build in a shared queue
   hipStream_t h2d = nullptr, comp[2] = {nullptr, nullptr};
@@ -50,25 +75,44 @@ struct HipBackend {
   uint32_t zerocopy_max = 1024;
 
   int init(const at2v_queue_opts& o) {
-    at2v_opts co{o.device, 1, o.policy, 0, 0, 0};
+    at2v_opts co{o.device, 1, o.policy, 0, 0, 0, o.cpu_threads, 0};
+    if (o.flags & AT2V_QUEUE_CPU) {
+      cpu_only = true;
+      co.num_gpus = 0;
+      return at2v_create(&co, &ctx);
+    }
     if (o.flags & AT2V_QUEUE_SENDER_COMB) {
       co.sender_cache = o.sender_cache ? o.sender_cache : 1024u;
       co.sender_comb = 1;
     }
-    const int rc = at2v_create(&co, &ctx);
+    int rc = at2v_create(&co, &ctx);
     if (rc) return rc;
+    if (o.flags & AT2V_QUEUE_CPU_FALLBACK) {
+      at2v_opts cc{0, 0, o.policy, 0, 0, 0, o.cpu_threads, 0};
+      rc = at2v_create(&cc, &cpu_ctx);
+      if (rc) return rc;
+    }
     device = o.device;
     if (const char* v = std::getenv("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
     if (const char* v = std::getenv("AT2V_QUEUE_ZEROCOPY")) zerocopy_max = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
-    if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
+    const DeviceScope scope(device);
+    if (scope.err != hipSuccess) return AT2V_E_HIP;
     if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     for (hipStream_t& c : comp)
       if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     return AT2V_OK;
   }
   void fini() {
-    if (hipSetDevice(device) == hipSuccess) {
+    at2v_destroy(cpu_ctx);
+    cpu_ctx = nullptr;
+    if (cpu_only) {
+      at2v_destroy(ctx);
+      ctx = nullptr;
+      return;
+    }
+    const DeviceScope scope(device);
+    if (scope.err == hipSuccess) {
       for (hipStream_t* s : {&h2d, &comp[0], &comp[1]})
         if (*s) {
           (void)hipStreamSynchronize(*s);
@@ -81,7 +125,6 @@ struct HipBackend {
   }
 
   int alloc(at2v::QueueSlot& s) {
-    if (hipSetDevice(device) != hipSuccess) return AT2V_E_HIP;
     DevSlot* d = new (std::nothrow) DevSlot;
     if (!d) return AT2V_E_OOM;
     s.backend = d;
@@ -89,6 +132,18 @@ struct HipBackend {
     const size_t cap = s.cap_records;
     d->msg_at = (cap * 100 + 4 + 15) / 16 * 16;  // pk, sig, off, then msg 16-byte aligned
     const size_t bytes = d->msg_at + s.cap_msg + 16;
+    if (cpu_only) {  // host memory only
+      d->host = static_cast<uint8_t*>(std::malloc(bytes));
+      s.verdicts = static_cast<uint32_t*>(std::malloc(words * 4));
+      if (!d->host || !s.verdicts) return AT2V_E_OOM;
+      s.pk = d->host;
+      s.sig = d->host + cap * 32;
+      s.off = reinterpret_cast<uint32_t*>(d->host + cap * 96);
+      s.msg = d->host + d->msg_at;
+      return AT2V_OK;
+    }
+    const DeviceScope scope(device);
+    if (scope.err != hipSuccess) return AT2V_E_HIP;
     bool ok = hipHostMalloc((void**)&d->host, bytes, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc((void**)&s.verdicts, words * 4, hipHostMallocDefault) == hipSuccess &&
               hipMalloc((void**)&d->dev, bytes) == hipSuccess && hipMalloc(&d->ver, words * 4) == hipSuccess;
@@ -108,7 +163,17 @@ struct HipBackend {
     return ok ? AT2V_OK : AT2V_E_OOM;
   }
   void release(at2v::QueueSlot& s) {
-    (void)hipSetDevice(device);
+    if (cpu_only) {
+      std::free(s.verdicts);
+      DevSlot* d = static_cast<DevSlot*>(s.backend);
+      if (d) std::free(d->host);
+      delete d;
+      s.backend = nullptr;
+      s.pk = s.sig = s.msg = nullptr;
+      s.off = s.verdicts = nullptr;
+      return;
+    }
+    const DeviceScope scope(device);
     if (s.verdicts) (void)hipHostFree(s.verdicts);
     s.pk = s.sig = s.msg = nullptr;
     s.off = s.verdicts = nullptr;
@@ -124,10 +189,35 @@ struct HipBackend {
   }
   // H2D on h2d -> verify on comp[k % 2] (waits for its upload), verdict words written to pinned host memory (or a D2H
   // copy on the same comp stream with AT2V_QUEUE_DIRECT=0)
+  // the slot's records on the CPU backend (cpu_ctx for a fallback), verdicts into its host words
+  int verify_on_cpu(at2v::QueueSlot& s, at2v_ctx* c) {
+    return at2v_verify_batch(c, s.pk, s.sig, s.msg, s.off, s.n, s.verdicts);
+  }
+  // a batch the device failed: drain what the slot's stream may still write into its verdict words, then the CPU
+  int fall_back(at2v::QueueSlot& s, int rc) {
+    DevSlot* d = static_cast<DevSlot*>(s.backend);
+    if (!cpu_ctx) return rc;
+    {
+      const DeviceScope scope(device);
+      if (d->stream) (void)hipStreamSynchronize(d->stream);
+    }
+    d->cpu_done = true;
+    fallbacks.fetch_add(1, std::memory_order_relaxed);
+    return verify_on_cpu(s, cpu_ctx);
+  }
   int launch(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
+    d->cpu_done = false;
+    if (cpu_only) return verify_on_cpu(s, ctx);
+    const int rc = launch_gpu(s);
+    return rc == AT2V_OK ? rc : fall_back(s, rc);
+  }
+  int launch_gpu(at2v::QueueSlot& s) {
+    DevSlot* d = static_cast<DevSlot*>(s.backend);
     hipStream_t comp = this->comp[launches++ & 1];
-    hipError_t e = hipSetDevice(device);
+    d->stream = comp;
+    const DeviceScope scope(device);
+    hipError_t e = scope.err;
     const size_t n = s.n, words = (n + 31) / 32;
     if (n <= zerocopy_max) {  // the kernel reads the pinned host buffers (same layout) directly
       uint32_t* ver = direct ? s.verdicts : (uint32_t*)d->ver;
@@ -159,6 +249,11 @@ struct HipBackend {
   }
   int wait(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
+    if (cpu_only || d->cpu_done) return AT2V_OK;  // verified in launch()
+    const int rc = wait_gpu(d);
+    return rc == AT2V_OK ? rc : fall_back(s, rc);
+  }
+  int wait_gpu(DevSlot* d) {
     if (spin_us) {
       const auto t0 = std::chrono::steady_clock::now();
       for (unsigned k = 0;; ++k) {
@@ -193,7 +288,7 @@ extern "C" {
 int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
-  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0, 0};
+  at2v_queue_opts o{0, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0, 0, 0};
   if (opts) o = *opts;
   at2v::QueueOpts qo;
   if (o.max_batch) qo.max_batch = o.max_batch;
@@ -202,7 +297,9 @@ int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (o.depth) qo.depth = (int)o.depth;
   qo.eager = (o.flags & AT2V_QUEUE_EAGER) != 0;
   if (const char* v = std::getenv("AT2V_QUEUE_LAUNCH_HERE")) qo.launch_here = std::atoi(v) != 0;  // (A/B)
-  if (o.flags & ~(AT2V_QUEUE_EAGER | AT2V_QUEUE_SENDER_COMB)) return AT2V_E_INVALID;
+  if (o.flags & ~(AT2V_QUEUE_EAGER | AT2V_QUEUE_SENDER_COMB | AT2V_QUEUE_CPU | AT2V_QUEUE_CPU_FALLBACK))
+    return AT2V_E_INVALID;
+  if ((o.flags & AT2V_QUEUE_CPU) && (o.flags & (AT2V_QUEUE_SENDER_COMB | AT2V_QUEUE_CPU_FALLBACK))) return AT2V_E_INVALID;
   if (qo.depth < 2 || qo.max_batch >= (1u << 31) || (uint64_t)qo.max_batch * qo.max_msg_bytes >= (1ull << 32))
     return AT2V_E_INVALID;
   at2v_queue* q = new (std::nothrow) at2v_queue;
@@ -257,6 +354,7 @@ int at2v_queue_get_stats(at2v_queue* q, at2v_queue_stats* out) {
   out->p50_us = s.p50_us;
   out->p99_us = s.p99_us;
   out->max_us = s.max_us;
+  out->cpu_fallbacks = q->be.fallbacks.load(std::memory_order_relaxed);
   return AT2V_OK;
 }
 

@@ -514,7 +514,7 @@ __device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t 
 // the entry's key and meta {0, valid 0, u, epoch}; claims that got a payload are appended to the launch's claim set for
 // the build stream. A claim that finds the free list empty (u = -1) or a record whose probe path is full flags the cache
 // full (compaction before the next launch). Returns the entry slot or -1.
-__device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t a[8], int lane) {
+__device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t a[8], int lane, bool active = true) {
   const uint32_t mask = c.cap - 1;
   int slot = -1, claimed = 0, found = 0, want = 0;
   uint64_t fp = cache_fingerprint(a, c.seed, c.fp_mask);
@@ -532,7 +532,15 @@ __device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t 
       break;
     }
   }
-  int leader = lane;
+  // a lane past the end of the batch (it recomputes the last record) looks up but neither claims nor counts as a sighting
+  if (!active) want = 0;
+  // a lane whose key is deferred (no claims while a compaction runs, or a first sighting) is a plain miss, not a failure
+  int deferred = 0;
+  if (c.no_claim && want) {  // a compaction is running: look up only (the records of a new key are misses)
+    want = 0;
+    deferred = 1;
+  }
+  int leader = lane, nsame = 0;
   {
     uint64_t pending = __ballot(want);
     while (pending) {  // one iteration per distinct wanted key in the wave
@@ -540,12 +548,29 @@ __device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t 
       const uint64_t fpL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fp >> 32), L) << 32) |
                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fp, L);
       const int same = want && fp == fpL;
-      if (same) leader = L;
-      pending &= ~__ballot(same);
+      const uint64_t sm = __ballot(same);
+      if (same) {
+        leader = L;
+        nsame = __popcll(sm);
+      }
+      pending &= ~sm;
     }
   }
   const int follower = want && leader != lane;
-  if (want && !follower) {  // phase 2: claim along the probe path (a racing claimant may take the tag first)
+  // admission: the wave's leader of a new key claims it only at its second sighting (or with 2+ records in this wave)
+  int sighted = 0;
+  if (want && !follower && !c.admit_first && nsame < 2) {
+    unsigned long long* sp = c.seen + ((uint32_t)(fp >> 40) & c.seen_mask);
+    if (__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fp) {
+      __hip_atomic_store(sp, (unsigned long long)fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sighted = 1;
+    }
+  }
+  {
+    const int ls = __shfl(sighted, leader);  // (every lane takes part in the shuffle)
+    if (want && ls) deferred = 1;
+  }
+  if (want && !follower && !sighted) {  // phase 2: claim along the probe path (a racing claimant may take the tag first)
     for (; k < 32; ++k) {
       const uint32_t j = (h + k) & mask;
       const unsigned long long old = atomicCAS(c.tags + j, 0ull, (unsigned long long)fp);
@@ -580,13 +605,15 @@ __device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t 
     if (q < fc) u = (int)c.free_slots[q];
   }
   const uint64_t pm = __ballot(claimed && u >= 0);
-  const uint64_t fm = __ballot(found), xm = __ballot(slot < 0);
+  // (a tail lane past n is no failure either: it must not flag the cache full)
+  const uint64_t fm = __ballot(found), xm = __ballot(slot < 0 && !deferred && active), sgm = __ballot(sighted);
   unsigned long long nbase = 0;
   if (lane == 0) {
     if (pm) nbase = atomicAdd(c.ctl + c.count_word, (unsigned long long)__popcll(pm));
     if (cm) atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
     if (fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
     if (xm) atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
+    if (sgm) atomicAdd(c.ctl + kCtlSighted, (unsigned long long)__popcll(sgm));
     if (cm != pm || xm) atomicExch(c.ctl + kCtlFull, 1ull);
   }
   nbase = __shfl(nbase, 0);
@@ -726,7 +753,7 @@ __device__ AT2V_INLINE void verify_chunks(
     if (kCache) {
       const CacheArgs& cc = *cp;
       // the chunk's senders: looked up (new keys claimed for the build stream) in the chunk prologue
-      const int slot = cache_lookup_wave(cc, Aw, lane);
+      const int slot = cache_lookup_wave(cc, Aw, lane, i < n);
       int a_ok = 0, u = 0;
       const bool hit = cache_hit(cc, slot, Aw, a_ok, u);
       const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
@@ -855,7 +882,7 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
     load8(Sw, sig + (size_t)ii * 64 + 32);
     load8(Aw, pk + (size_t)ii * 32);
     if (w == 0) {
-      const int slot = cache_lookup_wave(c, Aw, lane);
+      const int slot = cache_lookup_wave(c, Aw, lane, i < n);
       int a_ok0 = 0, u0 = 0;
       const bool hit0 = cache_hit(c, slot, Aw, a_ok0, u0);
       sent[lane] = hit0 ? u0 : -1;
@@ -1082,9 +1109,9 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
     {  // both halves' senders looked up (new keys claimed for the build stream) in the chunk prologue
       uint32_t Aw[8];
       load8(Aw, pk + (size_t)(i0 < n ? i0 : n - 1) * 32);
-      hit = cache_hit(cc, cache_lookup_wave(cc, Aw, lane), Aw, a_ok0, cidx0) ? 1 : 0;
+      hit = cache_hit(cc, cache_lookup_wave(cc, Aw, lane, i0 < n), Aw, a_ok0, cidx0) ? 1 : 0;
       load8(Aw, pk + (size_t)(i1 < n ? i1 : n - 1) * 32);
-      hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane), Aw, a_ok1, cidx1) ? 1 : 0;
+      hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane, i1 < n), Aw, a_ok1, cidx1) ? 1 : 0;
     }
     const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
     if (lane == 0) {
@@ -1183,7 +1210,7 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
       uint32_t Aw[8];
       const uint32_t iq = clamp(i0 + 64 * q);
       load8(Aw, pk + (size_t)iq * 32);
-      hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane), Aw, a_ok[q], cidx[q]) ? 1 : 0;
+      hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane, i0 + 64 * q < n), Aw, a_ok[q], cidx[q]) ? 1 : 0;
     }
     const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
     if (lane == 0) {
@@ -1562,7 +1589,8 @@ __device__ AT2V_INLINE void gen_msg_block(uint32_t out16[16], uint64_t cfg, uint
 }
 
 __global__ __launch_bounds__(kBlock) void gen_kernel(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len,
-                                                     uint64_t senders, uint8_t* __restrict__ pk,
+                                                     uint64_t senders, const uint64_t* __restrict__ keys,
+                                                     uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sig, uint8_t* __restrict__ msg,
                                                      uint32_t* __restrict__ off) {
   __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
@@ -1572,7 +1600,8 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(uint64_t cfg, uint64_t firs
   if (i >= n) return;
   const uint64_t idx = first + i;
   uint32_t seed[8];
-  gen_seed(seed, cfg, senders ? idx % senders : idx);  // key of sender idx % senders; M_i stays per record
+  // the key of seed index keys[i] (at2v_gen_records_keys_device), or of sender idx % senders; M_i stays per record
+  gen_seed(seed, cfg, keys ? keys[i] : senders ? idx % senders : idx);
   // message bytes into the output buffer (byte stores; msg_len arbitrary)
   uint8_t* m = msg + (size_t)i * msg_len;
   for (uint32_t ctr = 0; ctr * 64 < msg_len; ++ctr) {
@@ -1706,6 +1735,7 @@ __device__ AT2V_INLINE unsigned long long claim_count(const CacheArgs& c) {
 // Tables (combs off): one lane per claim of the set: dalek's decode verdict and [j]A (build_a_table, the verify
 // kernel's own steps) into payload u; the key comes from the entry the claim wrote.
 __global__ __launch_bounds__(256) void cache_build_kernel(CacheArgs c) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) c.ctl[kCtlBuildT0] = wall_clock64();  // (a vector store from one lane)
   const unsigned long long cnt = claim_count(c);
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < cnt; t += gridDim.x * 256) {
     const uint4 e = c.new_list[t];
@@ -1756,6 +1786,7 @@ __device__ AT2V_INLINE void comb_claim(const CacheArgs& c, uint32_t t, int g) {
 // position (profiles/r03zf); more claims, one wave per claim and 2 lanes per position (fewer redundant position chains
 // once the waves outnumber the SIMDs).
 __global__ __launch_bounds__(256) void cache_comb_kernel(CacheArgs c) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) c.ctl[kCtlBuildT0] = wall_clock64();  // (a vector store from one lane)
   const unsigned long long cnt = claim_count(c);
   if (cnt <= (unsigned long long)kCombWideMaxKeys) {
     for (uint32_t t = blockIdx.x; t < cnt; t += gridDim.x) comb_claim<kCombWideLog2>(c, t, (int)threadIdx.x);
@@ -1776,7 +1807,13 @@ __global__ __launch_bounds__(1024) void cache_flip_kernel(CacheArgs c) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(c.ctl + c.count_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    if (cnt) {  // the pass's device time (from the build kernel's first block to here) and its payload count
+      c.ctl[kCtlBuildTicks] += wall_clock64() - c.ctl[kCtlBuildT0];
+      c.ctl[kCtlBuilt] += cnt;
+    }
+    __hip_atomic_store(c.ctl + c.count_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // a fresh cache: every payload index free
@@ -2035,11 +2072,11 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   return hipGetLastError();
 }
 
-hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders, uint8_t* pk,
-                      uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream) {
+hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders,
+                      const uint64_t* keys, uint8_t* pk, uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(gen_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, cfg, first, n, msg_len,
-                     senders, pk, sig, msg, off);
+                     senders, keys, pk, sig, msg, off);
   return hipGetLastError();
 }
 

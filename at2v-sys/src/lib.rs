@@ -4,8 +4,8 @@
 //! Where it plugs into the reference (/root/reference, at2-node v1):
 //!   * per payload, as the body of drop's `Signature::verify` that sieve/murmur call for every payload
 //!     broadcast at src/bin/server/rpc.rs:275-284 -> `verify_one` (CPU, reentrant);
-//!   * per gossiped batch, ahead of `deliver()` at rpc.rs:156-173 -> `BatchVerifier::verify` (GPU) or the
-//!     ingest queue (`at2v_queue_*`);
+//!   * per gossiped batch, ahead of `deliver()` at rpc.rs:156-173 -> `BatchVerifier::verify` (GPU, or the CPU
+//!     backend on a node without one: `BatchVerifier::cpu`) or the ingest queue (`at2v_queue_*`);
 //!   * one process per GPU: `at2v_comm_init_rank` + `at2v_verify_batch_sharded` (RCCL all-gather of the
 //!     verdict bitmap over xGMI).
 //! The extern block below must stay identical to include/at2v.h (names, argument counts, integer widths);
@@ -31,7 +31,7 @@ pub struct At2vLedger {
 
 /// include/at2v.h AT2V_ABI_VERSION: the layouts of the #[repr(C)] structs below. `BatchVerifier::new` and
 /// `Queue::new` refuse a library that reports another version (the structs are copied whole by the library).
-pub const AT2V_ABI_VERSION: c_int = 5;
+pub const AT2V_ABI_VERSION: c_int = 6;
 
 pub const AT2V_POLICY_DALEK_V1: c_int = 0;
 pub const AT2V_POLICY_LIBSODIUM_1_0_18: c_int = 1;
@@ -67,11 +67,13 @@ pub const AT2V_VERDICT_INVALID: u8 = 0;
 pub const AT2V_VERDICT_VALID: u8 = 1;
 pub const AT2V_VERDICT_FAILED: u8 = 0xff;
 
-/// `Default`: device 0, one GPU, DALEK_V1, library-default small-batch threshold, no sender cache.
+/// `Default`: device 0, one GPU, DALEK_V1, library-default small-batch threshold, no sender cache, no CPU fallback.
+/// (Not derived: `num_gpus = 0` selects the CPU batch backend since ABI version 6.)
 #[repr(C)]
-#[derive(Clone, Copy, Debug, Default)]
+#[derive(Clone, Copy, Debug)]
 pub struct At2vOpts {
     pub device: c_int,
+    /// devices `device..device+num_gpus-1`; 0 = the CPU batch backend (no device, `cpu_threads` host threads)
     pub num_gpus: c_int,
     pub policy: c_int,
     /// launches of at most this many records run the low-latency kernel; 0 = 32768, AT2V_SMALL_BATCH_OFF = never
@@ -80,7 +82,23 @@ pub struct At2vOpts {
     pub sender_cache: u32,
     /// with sender_cache: 1 = per-key combs (all-hit chunks verify by table additions only); 0 = off
     pub sender_comb: u32,
+    /// host threads of the CPU backend (num_gpus = 0, or AT2V_CTX_CPU_FALLBACK); 0 = every usable CPU
+    pub cpu_threads: u32,
+    /// AT2V_CTX_CPU_FALLBACK | AT2V_CTX_ADMIT_FIRST
+    pub flags: u32,
 }
+
+impl Default for At2vOpts {
+    fn default() -> Self {
+        At2vOpts { device: 0, num_gpus: 1, policy: AT2V_POLICY_DALEK_V1, small_batch_max: 0, sender_cache: 0,
+                   sender_comb: 0, cpu_threads: 0, flags: 0 }
+    }
+}
+
+/// `At2vOpts::flags`: a GPU context re-runs a failed host-buffer batch on the CPU backend (same verdicts).
+pub const AT2V_CTX_CPU_FALLBACK: u32 = 1;
+/// `At2vOpts::flags`: sender-cache keys claim a payload at their first sighting (default: the second).
+pub const AT2V_CTX_ADMIT_FIRST: u32 = 2;
 
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
 pub const AT2V_SMALL_BATCH_OFF: u32 = 0xffffffff;
@@ -104,6 +122,12 @@ pub struct At2vInfo {
     pub cache_claims: u64,
     pub cache_evicted: u64,
     pub cache_compactions: u64,
+    pub cpu_threads: u64,
+    pub cpu_batches: u64,
+    pub cpu_fallbacks: u64,
+    pub cache_sightings: u64,
+    pub cache_built: u64,
+    pub cache_build_us: u64,
 }
 
 /// `Default`: device 0, DALEK_V1, and the library defaults for every size (65536 records, 1 ms, 256 B, depth 3).
@@ -117,13 +141,19 @@ pub struct At2vQueueOpts {
     pub max_msg_bytes: u32,
     pub depth: u32,
     pub flags: u32,
-    /// with AT2V_QUEUE_SENDER_COMB: keys the queue's context caches (2.1 MB of HBM each); 0 = 1024
+    /// with AT2V_QUEUE_SENDER_COMB: keys the queue's context caches (HBM per key: see include/at2v.h); 0 = 1024
     pub sender_cache: u32,
+    /// AT2V_QUEUE_CPU / AT2V_QUEUE_CPU_FALLBACK: host threads (0 = every usable CPU)
+    pub cpu_threads: u32,
 }
 
 /// `At2vQueueOpts::flags`: also seal the filling batch whenever no batch is in flight (latency mode).
 pub const AT2V_QUEUE_EAGER: u32 = 1;
 pub const AT2V_QUEUE_SENDER_COMB: u32 = 2;
+/// `At2vQueueOpts::flags`: batches verified by the CPU backend (no device).
+pub const AT2V_QUEUE_CPU: u32 = 4;
+/// `At2vQueueOpts::flags`: a batch the device fails is verified on the CPU backend instead.
+pub const AT2V_QUEUE_CPU_FALLBACK: u32 = 8;
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
@@ -136,6 +166,7 @@ pub struct At2vQueueStats {
     pub p50_us: f64,
     pub p99_us: f64,
     pub max_us: f64,
+    pub cpu_fallbacks: u64,
 }
 
 #[repr(C)]
@@ -193,6 +224,9 @@ extern "C" {
     pub fn at2v_gen_records_senders_device(ctx: *mut At2vCtx, cfg_seed: u64, first: u64, n: usize, msg_len: u32,
                                            senders: u64, d_pk: *mut u8, d_sig: *mut u8, d_msg: *mut u8,
                                            d_msg_off: *mut u32, hip_stream: *mut c_void) -> c_int;
+    pub fn at2v_gen_records_keys_device(ctx: *mut At2vCtx, cfg_seed: u64, first: u64, n: usize, msg_len: u32,
+                                        d_keys: *const u64, d_pk: *mut u8, d_sig: *mut u8, d_msg: *mut u8,
+                                        d_msg_off: *mut u32, hip_stream: *mut c_void) -> c_int;
     pub fn at2v_sign_batch(ctx: *mut At2vCtx, seeds: *const u8, msg: *const u8, msg_off: *const u32, n: usize,
                            pk_out: *mut u8, sig_out: *mut u8) -> c_int;
     pub fn at2v_get_info(ctx: *mut At2vCtx, out: *mut At2vInfo) -> c_int;
@@ -286,8 +320,8 @@ fn check_abi() -> Result<(), Error> {
     Ok(())
 }
 
-/// Owner of an at2v context (GPU). Not Sync: one thread at a time; call from `spawn_blocking` or a
-/// dedicated thread, never on an async executor thread.
+/// Owner of an at2v context (GPUs, or the CPU backend). Not Sync: one thread at a time; call from `spawn_blocking` or
+/// a dedicated thread, never on an async executor thread.
 pub struct BatchVerifier(*mut At2vCtx);
 
 unsafe impl Send for BatchVerifier {}
@@ -303,6 +337,12 @@ impl BatchVerifier {
     /// `num_gpus` devices from `device` on, library defaults otherwise.
     pub fn on_devices(device: i32, num_gpus: i32, policy: c_int) -> Result<Self, Error> {
         Self::new(&At2vOpts { device, num_gpus, policy, ..Default::default() })
+    }
+
+    /// The CPU batch backend (a node without a gfx950): `cpu_threads` host threads (0 = every usable CPU) over the
+    /// kernels' own verify routine; the drop-in for the reference's `num_cpus::get()` verify workers (rpc.rs:124-125).
+    pub fn cpu(cpu_threads: u32, policy: c_int) -> Result<Self, Error> {
+        Self::new(&At2vOpts { num_gpus: 0, policy, cpu_threads, ..Default::default() })
     }
 
     /// One process per GPU: join the node's RCCL communicator (collective over `world` ranks).

@@ -26,12 +26,15 @@ extern "C" {
 #endif
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
- * version 5 appended at2v_queue_opts.sender_cache and at2v_info.cache_capacity / cache_claims / cache_evicted /
+ * version 6 appended at2v_opts.cpu_threads / flags (num_gpus = 0 now means the CPU batch backend, no device),
+ * at2v_info.cpu_threads / cpu_batches / cpu_fallbacks / cache_sightings / cache_built / cache_build_us,
+ * at2v_gen_records_keys_device, at2v_queue_opts.cpu_threads (with the
+ * AT2V_QUEUE_CPU / AT2V_QUEUE_CPU_FALLBACK flags) and at2v_queue_stats.cpu_fallbacks; version 5 appended at2v_queue_opts.sender_cache and at2v_info.cache_capacity / cache_claims / cache_evicted /
  * cache_compactions (the sender cache replaces entries instead of restarting empty); version 4 appended
  * at2v_opts.sender_comb and the AT2V_QUEUE_SENDER_COMB queue flag; version 3 appended at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
  * at2v_opts.small_batch_max and at2v_queue_opts.flags). A binding checks at2v_abi_version() == AT2V_ABI_VERSION
  * before passing any struct (the Python and Rust bindings in this repo refuse a mismatching library). */
-#define AT2V_ABI_VERSION 5
+#define AT2V_ABI_VERSION 6
 int at2v_abi_version(void);
 
 typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, and the RCCL
@@ -44,7 +47,9 @@ typedef enum {
 
 typedef struct {
   int device;         /* first HIP device ordinal (default 0) */
-  int num_gpus;       /* devices device..device+num_gpus-1 share each host batch by index range; 0 or 1 = one GPU */
+  int num_gpus;       /* devices device..device+num_gpus-1 share each host batch by index range. 0 = the CPU batch
+                         backend: no device is touched; at2v_verify_batch runs the kernels' own verify routine on
+                         cpu_threads host threads (what SystemManager::run(.., num_cpus::get()) did, rpc.rs:124-125) */
   at2v_policy policy; /* verdict semantics */
   uint32_t small_batch_max; /* launches of at most this many records run the low-latency kernel (two lanes per
                                record, one wave per SIMD); 0 = 32768; AT2V_SMALL_BATCH_OFF = never */
@@ -60,7 +65,18 @@ typedef struct {
                                64-record chunk whose senders are all cached is verified by 42 table additions and one
                                inversion instead of the doubling ladder (~3x fewer multiplications; launches of any size,
                                small batches included). Same verdicts. 0 = off. */
+  uint32_t cpu_threads;     /* host threads of the CPU backend (num_gpus = 0, or AT2V_CTX_CPU_FALLBACK): 0 = every CPU
+                               this process may use (affinity mask, capped by a cgroup CPU quota) */
+  uint32_t flags;           /* AT2V_CTX_* below */
 } at2v_opts;
+/* A GPU context that hits a device error inside at2v_verify_batch (host buffers: the records are still on the host)
+ * verifies that batch again on the CPU backend and returns AT2V_OK with identical verdicts; at2v_info.cpu_fallbacks counts
+ * it. Device-buffer entry points cannot fall back (their records live on the failed device) and return the error. */
+#define AT2V_CTX_CPU_FALLBACK 1u
+/* Sender cache admission: by default a key gets a cache payload (a [j]A table, or a 1.7 MB comb) only when it is seen
+ * again in a later launch, or when one wave of a launch holds two or more of its records, so one-shot senders cost a
+ * sighting (one 8-byte store) instead of a build. This flag admits every key at its first sighting (round-4 behaviour). */
+#define AT2V_CTX_ADMIT_FIRST 2u
 #define AT2V_SMALL_BATCH_DEFAULT 32768u
 #define AT2V_SMALL_BATCH_OFF 0xffffffffu
 
@@ -96,7 +112,8 @@ void at2v_destroy(at2v_ctx* ctx);
 int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                       const uint32_t* msg_off, size_t n, uint32_t* verdicts);
 
-/* Batch verify on device-resident buffers of ctx's first device, asynchronously on `hip_stream`
+/* Batch verify on device-resident buffers of ctx's first device (AT2V_E_NODEVICE on a CPU context), asynchronously on
+ * `hip_stream`
  * (a hipStream_t; NULL = the null stream). Same layout as at2v_verify_batch; msg_bytes = size of the
  * msg buffer in bytes (>= msg_off[n]); d_pk/d_sig 16-byte aligned, d_msg_off/d_verdicts 4-byte aligned.
  * Returns after the launch; results are valid once the stream reaches this point. The ceil(n/32) verdict
@@ -112,7 +129,8 @@ int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* 
  * ("CPU, 1/0"), for callers that verify one payload at a time, e.g. the A/sig decode at
  * rpc.rs:265-281. DALEK_V1 semantics: the throughput kernel's own verify routine (csrc/at2v_verify_fu.h)
  * compiled for the host; needs no GPU, no context and no lock; reentrant (the first call of a process builds the
- * fixed-base tables, ~30 ms). It is not a fallback of the batch entry points: they never verify on the CPU. */
+ * fixed-base tables, ~30 ms). A CPU context (num_gpus = 0) and the AT2V_CTX_CPU_FALLBACK path run the same routine
+ * over a thread pool. */
 int at2v_verify_one(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len);
 /* Same, with an explicit policy (AT2V_POLICY_*). */
 int at2v_verify_one_policy(const uint8_t pk[32], const uint8_t sig[64], const uint8_t* msg, size_t len, int policy);
@@ -136,6 +154,12 @@ int at2v_gen_records_senders_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t f
                                     uint64_t senders, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
                                     uint32_t* d_msg_off, void* hip_stream);
 
+/* The same with an explicit key per record: record i is signed by the key of seed index d_keys[i] (n u64 on the device,
+ * 8-byte aligned), its message is still M_(first+i). For traffic with a chosen sender distribution (bench: Zipf). */
+int at2v_gen_records_keys_device(at2v_ctx* ctx, uint64_t cfg_seed, uint64_t first, size_t n, uint32_t msg_len,
+                                 const uint64_t* d_keys, uint8_t* d_pk, uint8_t* d_sig, uint8_t* d_msg,
+                                 uint32_t* d_msg_off, void* hip_stream);
+
 /* RFC 8032 signing of host messages under 32-byte seeds (host buffers, synchronous). pk_out n x 32,
  * sig_out n x 64. The GPU counterpart of KeyPair::sign (drop), used by tests and the bench generator. */
 int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, const uint32_t* msg_off, size_t n,
@@ -143,7 +167,7 @@ int at2v_sign_batch(at2v_ctx* ctx, const uint8_t* seeds, const uint8_t* msg, con
 
 /* Introspection for benches: kernel geometry actually used by the last verify launch. */
 typedef struct {
-  int num_gpus;
+  int num_gpus;        /* 0: a CPU-backend context (the geometry fields below are then 0) */
   int grid_blocks;     /* per device */
   int block_threads;
   int waves_per_cu;    /* resident waves per CU admitted by the kernel's register/LDS use */
@@ -159,6 +183,12 @@ typedef struct {
   uint64_t cache_claims;     /* keys claimed (first seen, or seen again after being replaced) */
   uint64_t cache_evicted;    /* entries replaced to make room */
   uint64_t cache_compactions;/* replacement passes */
+  uint64_t cpu_threads;      /* threads of the context's CPU backend (0: none) */
+  uint64_t cpu_batches;      /* batches verified on the CPU backend (a CPU context's batches, and fallbacks) */
+  uint64_t cpu_fallbacks;    /* ... of which a GPU context re-ran after a device error (AT2V_CTX_CPU_FALLBACK) */
+  uint64_t cache_sightings;  /* first sightings recorded instead of claiming a payload (admission, AT2V_CTX_ADMIT_FIRST) */
+  uint64_t cache_built;      /* payloads (tables or combs) built */
+  uint64_t cache_build_us;   /* device time of the build passes that built something (first build block to the flip) */
 } at2v_info;
 /* With a sender cache, at2v_get_info first waits for the context's cache work (its build stream, which follows every
  * cached launch and therefore waits for those launches, and whatever each launch's stream ran before them). */
@@ -219,13 +249,18 @@ typedef struct {
                              per-sender combs (at2v_opts.sender_comb) */
   uint32_t sender_cache;  /* with AT2V_QUEUE_SENDER_COMB: keys the queue's context caches (at2v_opts.sender_cache,
                              1.7 MB of HBM each); 0 = 1024 */
+  uint32_t cpu_threads;   /* AT2V_QUEUE_CPU / AT2V_QUEUE_CPU_FALLBACK: host threads (0 = every usable CPU) */
 } at2v_queue_opts;
 #define AT2V_QUEUE_EAGER 1u
 #define AT2V_QUEUE_SENDER_COMB 2u /* the queue's context gets a sender cache (sender_cache keys) with sender_comb = 1 */
+#define AT2V_QUEUE_CPU 4u         /* batches verified by the CPU backend (a context with num_gpus = 0): no device */
+#define AT2V_QUEUE_CPU_FALLBACK 8u /* a batch whose launch or completion fails on the device is verified on the CPU
+                                     backend instead (the slot's records are in host memory); same verdicts */
 typedef struct {
   uint64_t submitted, completed, batches, failed_batches;
   double mean_batch;           /* records per completed batch */
   double p50_us, p99_us, max_us; /* submit -> verdict published, per record (since create / reset) */
+  uint64_t cpu_fallbacks;        /* AT2V_QUEUE_CPU_FALLBACK: batches the device failed and the CPU backend verified */
 } at2v_queue_stats;
 int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out);
 void at2v_queue_destroy(at2v_queue* q); /* seals and completes everything submitted, then frees */

@@ -38,7 +38,13 @@ class Oracle:
         L.oracle_point_add.argtypes = [P, P, P]
         L.oracle_point_add.restype = ctypes.c_int
         L.oracle_small_order_encoding.argtypes = [ctypes.c_int, P]
+        L.oracle_decompress_ok.argtypes = [P]
+        L.oracle_decompress_ok.restype = ctypes.c_int
         self.L = L
+
+    def decompress_ok(self, p: bytes) -> bool:
+        """dalek CompressedEdwardsY::decompress succeeds (SURVEY Appendix A V2)"""
+        return bool(self.L.oracle_decompress_ok(bytes(p)))
 
     @staticmethod
     def _p(a):

@@ -199,12 +199,13 @@ def test_repeat_determinism(verifier, golden):
     assert np.array_equal(a, b)
 
 
-def test_multi_gpu_context_if_available(at2v_mod, golden):
+def test_multi_gpu_context(at2v_mod, golden, monkeypatch):
+    """one context over 8 devices; on a box with fewer, the test hook AT2V_TEST_DEVICE_ALIAS maps shard g to device
+    g % ndev so the single-process split still runs (tests/test_gpu_multidev.py has the full matrix)"""
     import torch
-    ng = torch.cuda.device_count()
-    if ng < 2:
-        pytest.skip("single GPU box")
-    v = at2v_mod.BatchVerifier(num_gpus=ng)
+    if torch.cuda.device_count() < 8:
+        monkeypatch.setenv("AT2V_TEST_DEVICE_ALIAS", "1")
+    v = at2v_mod.BatchVerifier(num_gpus=8)
     g = golden["adversarial"]
     assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek)
     v.close()

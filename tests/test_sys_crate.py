@@ -150,7 +150,7 @@ def _struct_literals(src: str):
     (struct name, named fields, base expression or None). Handles `field: expr`, shorthand `field` and `..base`."""
     for m in re.finditer(r"(?<![\w])(At2v\w+)\s*\{", src):
         before = src[max(0, m.start() - 12):m.start()]
-        if re.search(r"struct\s+$", before):
+        if re.search(r"(struct|for|impl)\s+$", before):  # a definition or an `impl Trait for At2vX {` block
             continue
         i, depth = m.end(), 1
         while depth:
@@ -182,7 +182,9 @@ def _struct_literals(src: str):
 
 
 def _default_structs(src: str):
-    return set(re.findall(r"#\[derive\([^)]*\bDefault\b[^)]*\)\]\s*pub struct (At2v\w+)", src))
+    """structs with a Default: derived, or a hand-written `impl Default for` (At2vOpts since ABI v6: num_gpus = 1)"""
+    return (set(re.findall(r"#\[derive\([^)]*\bDefault\b[^)]*\)\]\s*pub struct (At2v\w+)", src))
+            | set(re.findall(r"impl\s+Default\s+for\s+(At2v\w+)", src)))
 
 
 def check_struct_literals(src: str, fields: dict, defaults: set):

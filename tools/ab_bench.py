@@ -14,9 +14,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import at2v  # noqa: E402
 
 
-class Opts(ctypes.Structure):  # include/at2v.h at2v_opts (ABI v4)
+class Opts(ctypes.Structure):  # include/at2v.h at2v_opts (ABI v6)
     _fields_ = [("device", ctypes.c_int), ("num_gpus", ctypes.c_int), ("policy", ctypes.c_int),
-                ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32), ("sender_comb", ctypes.c_uint32)]
+                ("small_batch_max", ctypes.c_uint32), ("sender_cache", ctypes.c_uint32), ("sender_comb", ctypes.c_uint32),
+                ("cpu_threads", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
 def open_lib(path, comb=False):
@@ -27,7 +28,7 @@ def open_lib(path, comb=False):
     lib.at2v_gen_records_senders_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
                                                     ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P]
     h = P()
-    o = Opts(0, 1, 0, 0, 1024 if comb else 0, 1 if comb else 0)
+    o = Opts(0, 1, 0, 0, 1024 if comb else 0, 1 if comb else 0, 0, 0)
     assert lib.at2v_create(ctypes.byref(o), ctypes.byref(h)) == 0
     return lib, h
 
