@@ -81,7 +81,7 @@ class _Info(ctypes.Structure):
                 ("cache_compactions", ctypes.c_uint64), ("cpu_threads", ctypes.c_uint64),
                 ("cpu_batches", ctypes.c_uint64), ("cpu_fallbacks", ctypes.c_uint64),
                 ("cache_sightings", ctypes.c_uint64), ("cache_built", ctypes.c_uint64),
-                ("cache_build_us", ctypes.c_uint64)]
+                ("cache_build_us", ctypes.c_uint64), ("cache_record_hits", ctypes.c_uint64)]
 
 
 UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)

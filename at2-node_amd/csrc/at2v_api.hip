@@ -35,7 +35,8 @@
 namespace at2v {
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache);
+                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache,
+                         const PartArgs* part);
 size_t btab_bytes();
 hipError_t launch_build_btab(int4* out, hipStream_t stream);
 hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders,
@@ -124,6 +125,7 @@ struct Shard {
   int blocks_per_cu = 0;
   int vgprs = 0;
   DevBuf scratch[4];
+  DevBuf part[4];  // per scratch set: the classify kernel's hit / miss lists (partitioned cached launches)
   DevBuf btab, pk, sig, msg, off, verdict;
   hipEvent_t copied = nullptr;  // at2v_verify_batch: the verdict copy (the call waits for this, not for the builds)
   SenderCache* cache = nullptr;
@@ -142,6 +144,7 @@ struct at2v_ctx {
   at2v::CpuPool* cpu = nullptr;  // the CPU backend (a CPU context, or AT2V_CTX_CPU_FALLBACK)
   uint64_t cpu_batches = 0, cpu_fallbacks = 0;
   uint32_t test_fail_launches = 0;  // AT2V_TEST_FAIL_LAUNCH (tests only): that many launches fail before the kernel
+  bool partition = true;  // cached launches above pair_max classify, then verify hits and misses apart (AT2V_CACHE_PARTITION)
   ncclComm_t comm = nullptr;  // at2v_comm_init_rank (one rank per process, the context's first device)
   int rank = 0, world = 1;
   DevBuf window;              // at2v_verify_batch_sharded: world x kGatherWindow words, one all-gather round
@@ -381,9 +384,21 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
     c->args.epoch = (uint32_t)++c->launches;
     ca = c->args;
   }
+  at2v::PartArgs pa{};
+  const bool part = c && ctx->partition && n > ctx->pair_max;
+  if (e == hipSuccess && part) {
+    const size_t need = (size_t)n * at2v::part_bytes_per_record();
+    if (s.part[j].cap < need) {  // grows: the set's previous launch (it reads the old lists) must be done first
+      e = hipEventSynchronize(s.scratch_free[j]);
+      if (e == hipSuccess) e = s.part[j].ensure(need);
+    }
+    uint32_t* base = (uint32_t*)s.part[j].p;
+    pa = at2v::PartArgs{base, base + n, base + 2 * (size_t)n, nullptr};
+  }
   if (e == hipSuccess)
     e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch[j].p,
-                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &ca : nullptr);
+                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &ca : nullptr,
+                            part ? &pa : nullptr);
   if (e == hipSuccess && c) {
     // claims of this launch -> payloads on the build stream (later launches use them; this one did not wait)
     e = hipEventRecord(c->claims_ready[cs], stream);
@@ -476,6 +491,7 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   c->policy = o.policy;
   c->flags = o.flags;
   if (const char* v = std::getenv("AT2V_TEST_FAIL_LAUNCH")) c->test_fail_launches = (uint32_t)std::strtoul(v, nullptr, 10);
+  if (const char* v = std::getenv("AT2V_CACHE_PARTITION")) c->partition = std::atoi(v) != 0;  // (A/B: 0 = round 4)
   c->pair_max = o.small_batch_max == 0 ? AT2V_SMALL_BATCH_DEFAULT
                 : o.small_batch_max == AT2V_SMALL_BATCH_OFF ? 0u : o.small_batch_max;
   c->shards.resize((size_t)o.num_gpus);
@@ -534,6 +550,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     if (s.copied) (void)hipEventDestroy(s.copied);
     free_cache(s.cache);
     for (DevBuf& b : s.scratch) b.release();
+    for (DevBuf& b : s.part) b.release();
     s.btab.release();
     s.pk.release();
     s.sig.release();
@@ -950,6 +967,7 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
       out->cache_compactions += w[at2v::kCtlCompactions];
       out->cache_sightings += w[at2v::kCtlSighted];
       out->cache_built += w[at2v::kCtlBuilt];
+      out->cache_record_hits += w[at2v::kCtlRecHits];
       int khz = 0;  // device wall clock (wall_clock64) in kHz
       if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, sh.device) == hipSuccess && khz > 0)
         out->cache_build_us += w[at2v::kCtlBuildTicks] * 1000ull / (uint64_t)khz;

@@ -52,6 +52,20 @@ struct CacheArgs {
                              // stream: the launch reads the old table, claims nothing, so the free list stays intact)
 };
 
+// Partitioned cached launch (round 5, launches above small_batch_max): cache_classify_kernel looks every record's sender
+// up (claims, sightings, statistics) and splits the launch's record indices into a hit list (with each hit's payload
+// index and decode verdict) and a miss list; the comb kernel then verifies the hit list by comb additions, four records
+// per lane, and the ladder kernel the miss list (with [j]A tables: the hit list too, skipping A's decode). So a record
+// takes the cached path whenever ITS sender is cached, whatever the other records of its chunk; round 4 required all
+// 256 records of a chunk to hit, which mixed traffic (many senders) almost never does.
+struct PartArgs {
+  uint32_t* hidx;    // record indices of the hits (counts[0] of them, in no particular order)
+  uint32_t* hinfo;   // per hit: (payload index << 1) | dalek decode verdict of A
+  uint32_t* midx;    // record indices of the misses (counts[1])
+  uint32_t* counts;  // [0] hits, [1] misses (zeroed before the classify kernel)
+};
+size_t part_bytes_per_record();
+
 // compaction work buffers (one per device; the alternate tag/entry arrays are swapped in by the host)
 struct CacheCompactArgs {
   unsigned long long* new_tags;
@@ -86,6 +100,7 @@ enum CacheCtlWord : int {
   kCtlBuildT0,       // device wall clock (wall_clock64) when the current build pass started
   kCtlBuildTicks,    // wall-clock ticks of every build pass that built something (at2v_info.cache_build_us)
   kCtlBuilt,         // payloads built
+  kCtlRecHits,       // records whose sender was served from the cache (partitioned launches)
   kCtlHist,          // 64 age buckets
   kCtlWordsTotal = kCtlHist + 64
 };

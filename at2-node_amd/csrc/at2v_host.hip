@@ -73,6 +73,11 @@ struct HipBackend {
   // (one host-to-device copy and its cross-stream wait less on the latency path; config 5 queue p50 123-130 -> 109-117
   // us, p99 242-285 -> 154-187 us, profiles/r04w). AT2V_QUEUE_ZEROCOPY overrides (0 = always upload).
   uint32_t zerocopy_max = 1024;
+  // Compute streams the queue alternates over (AT2V_QUEUE_STREAMS, 1 or 2) and their priority (AT2V_QUEUE_PRIORITY = 1:
+  // the device's greatest stream priority). The host-to-device stream is created on the first batch that needs an
+  // upload (above zerocopy_max records), so a latency-mode node maps fewer hardware queues.
+  int ncomp = 2;
+  bool prio = false;
 
   int init(const at2v_queue_opts& o) {
     at2v_opts co{o.device, 1, o.policy, 0, 0, 0, o.cpu_threads, 0};
@@ -96,11 +101,17 @@ struct HipBackend {
     if (const char* v = std::getenv("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
     if (const char* v = std::getenv("AT2V_QUEUE_ZEROCOPY")) zerocopy_max = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
+    if (const char* v = std::getenv("AT2V_QUEUE_STREAMS")) ncomp = std::atoi(v) == 1 ? 1 : 2;
+    if (const char* v = std::getenv("AT2V_QUEUE_PRIORITY")) prio = std::atoi(v) != 0;
     const DeviceScope scope(device);
     if (scope.err != hipSuccess) return AT2V_E_HIP;
-    if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
-    for (hipStream_t& c : comp)
-      if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
+    int least = 0, greatest = 0;
+    if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) prio = false;
+    for (int k = 0; k < ncomp; ++k) {
+      const hipError_t e = prio ? hipStreamCreateWithPriority(&comp[k], hipStreamNonBlocking, greatest)
+                                : hipStreamCreateWithFlags(&comp[k], hipStreamNonBlocking);
+      if (e != hipSuccess) return AT2V_E_HIP;
+    }
     return AT2V_OK;
   }
   void fini() {
@@ -214,7 +225,7 @@ struct HipBackend {
   }
   int launch_gpu(at2v::QueueSlot& s) {
     DevSlot* d = static_cast<DevSlot*>(s.backend);
-    hipStream_t comp = this->comp[launches++ & 1];
+    hipStream_t comp = this->comp[ncomp == 2 ? (launches++ & 1) : 0];
     d->stream = comp;
     const DeviceScope scope(device);
     hipError_t e = scope.err;
@@ -228,6 +239,7 @@ struct HipBackend {
       if (e == hipSuccess) e = hipEventRecord(d->done, comp);
       return e == hipSuccess ? AT2V_OK : AT2V_E_HIP;
     }
+    if (!h2d && hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) return AT2V_E_HIP;
     if (d->msg_at + s.msg_used <= kSingleCopyMax) {  // one copy of the whole used span (small slots / latency mode)
       if (e == hipSuccess) e = hipMemcpyAsync(d->dev, d->host, d->msg_at + s.msg_used, hipMemcpyHostToDevice, h2d);
     } else {

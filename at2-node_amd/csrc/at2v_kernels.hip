@@ -645,6 +645,26 @@ __device__ AT2V_INLINE bool cache_hit(const CacheArgs& c, int slot, const uint32
   return hit;
 }
 
+// Verdict bits of a partitioned launch's wave (kPart: records in list order). When the wave's 64 records are 64
+// consecutive records starting at a multiple of 64 (a list segment appended by one classify wave whose records all went
+// to that list: the common case), lane 0 ORs two whole words; otherwise every valid record ORs its own bit. (64 atomics
+// on the same two words from one instruction serialise in L2: +20% on a 1M-record comb launch, profiles/r05e.)
+__device__ AT2V_INLINE void verdict_or(uint32_t* __restrict__ verdicts, uint32_t rec, int good, bool act, int lane) {
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rec);
+  const int contig = __builtin_amdgcn_readfirstlane(__all(act && rec == r0 + (uint32_t)lane) && (r0 & 63u) == 0 ? 1 : 0);
+  if (contig) {
+    const uint64_t m = __ballot(good);
+    if (lane == 0) {
+      if ((uint32_t)m)
+        __hip_atomic_fetch_or(verdicts + (r0 >> 5), (uint32_t)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(m >> 32))
+        __hip_atomic_fetch_or(verdicts + (r0 >> 5) + 1, (uint32_t)(m >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (good && act) {
+    __hip_atomic_fetch_or(verdicts + (rec >> 5), 1u << (rec & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Half-size verification: one chunk of 64 records per wave, no final inversion. kCache: the per-sender A
 // cache is on; a wave whose 64 records all hit it skips decoding A and building [j]A (slot_of / cache from
 // cache_lookup_kernel + cache_build_kernel, launched just before on the same stream).
@@ -652,18 +672,29 @@ __device__ AT2V_INLINE bool cache_hit(const CacheArgs& c, int slot, const uint32
 // round 2's signature and code (an extra-parameter template of it measured ~1% slower: profiles/r03b, r03d).
 // kComb (with kCache): entries carry per-key combs (at2v_comb.h); a wave whose 64 records all hit verifies from them
 // (additions only), any other wave runs the uncached half-size path.
-template <bool kCache, bool kComb = false>
+// kPart (partitioned cached launches, at2v_cache.h PartArgs): chunks are 64 entries of the classify kernel's lists
+// instead of 64 consecutive records: with kCache ([j]A tables) the hit list's chunks (every record cached: A's decode and
+// table skipped) and then the miss list's, without it the miss list alone (the comb kernel takes the hits). A record's
+// verdict bit is set by an atomic OR (the lists are in no particular order; the launcher zeroed the words).
+template <bool kCache, bool kComb = false, bool kPart = false>
 __device__ AT2V_INLINE void verify_chunks(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
     uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
-    uint32_t* __restrict__ chunk_queue, const CacheArgs* cp) {
+    uint32_t* __restrict__ chunk_queue, const CacheArgs* cp, const PartArgs* pp = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t nchunks = (n + 63) / 64;
+  uint32_t nchunks = (n + 63) / 64;
   const uint32_t nwords = (n + 31) / 32;
+  uint32_t nh = 0, nm = 0, hchunks = 0;
+  if constexpr (kPart) {  // the list sizes the classify kernel left (same stream: complete)
+    nh = kCache ? __builtin_amdgcn_readfirstlane(pp->counts[0]) : 0u;
+    nm = __builtin_amdgcn_readfirstlane(pp->counts[1]);
+    hchunks = (nh + 63) / 64;
+    nchunks = hchunks + (nm + 63) / 64;
+  }
 #ifndef AT2V_MSG_TOUCH
 #define AT2V_MSG_TOUCH 0  // 1: early loads of each lane's message sectors (consumed at SHA-512), see verify_chunks
 #endif
@@ -706,8 +737,22 @@ __device__ AT2V_INLINE void verify_chunks(
 #ifdef AT2V_WAIT_PROBE
     const unsigned long long t_chunk0 = __builtin_amdgcn_s_memtime();
 #endif
-    const uint32_t i = c * 64 + lane;
-    const uint32_t ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
+    uint32_t i, ii;
+    bool act;
+    int phit = 0;        // kPart: a hit-list chunk (wave-uniform)
+    uint32_t pinfo = 0;  // kPart: the hit's (payload << 1) | A's decode verdict
+    if constexpr (kPart) {
+      phit = c < hchunks ? 1 : 0;
+      const uint32_t pos = (phit ? c : c - hchunks) * 64 + lane, cnt = phit ? nh : nm;
+      const uint32_t pc = pos < cnt ? pos : cnt - 1;  // tail lanes recompute the list's last record; masked
+      act = pos < cnt;
+      i = ii = (phit ? pp->hidx : pp->midx)[pc];
+      if (phit) pinfo = pp->hinfo[pc];
+    } else {
+      i = c * 64 + lane;
+      ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
+      act = i < n;
+    }
     uint32_t Rw[8], Sw[8], Aw[8];
     load8(Rw, sig + (size_t)ii * 64);
     load8(Sw, sig + (size_t)ii * 64 + 32);
@@ -752,31 +797,37 @@ __device__ AT2V_INLINE void verify_chunks(
     int good;
     if (kCache) {
       const CacheArgs& cc = *cp;
-      // the chunk's senders: looked up (new keys claimed for the build stream) in the chunk prologue
-      const int slot = cache_lookup_wave(cc, Aw, lane, i < n);
-      int a_ok = 0, u = 0;
-      const bool hit = cache_hit(cc, slot, Aw, a_ok, u);
-      const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
-      if (lane == 0) {
-        atomicAdd(cc.ctl + kCtlChunks, 1ull);
-        if (all_hit) atomicAdd(cc.ctl + kCtlChunkHits, 1ull);
+      int a_ok = 0, u = 0, all_hit;
+      if constexpr (kPart) {  // classified already
+        all_hit = phit;
+        a_ok = (int)(pinfo & 1u);
+        u = (int)(pinfo >> 1);
+      } else {
+        // the chunk's senders: looked up (new keys claimed for the build stream) in the chunk prologue
+        const int slot = cache_lookup_wave(cc, Aw, lane, i < n);
+        const bool hit = cache_hit(cc, slot, Aw, a_ok, u);
+        all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
+        if (lane == 0) {
+          atomicAdd(cc.ctl + kCtlChunks, 1ull);
+          if (all_hit) atomicAdd(cc.ctl + kCtlChunkHits, 1ull);
+        }
       }
       if (kComb) {
         if (all_hit) {
           const DevComb tc{cc.payload + (size_t)u * (kCombBytes / 16), {astage + wib * 640, rstage + wib * 640}, lane};
           const DevBComb tbc{cc.bcomb, {astage + wib * 640, rstage + wib * 640}, lane};
-          good = verify_comb_fu(Rw, Aw, Sw, len, msgword, policy, a_ok, tc, tbc) & (i < n);
+          good = verify_comb_fu(Rw, Aw, Sw, len, msgword, policy, a_ok, tc, tbc) & act;
         } else {
-          good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+          good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & act;
         }
       } else {
         DevTabA tc{ta};
         if (all_hit) tc.base = cc.payload + (size_t)u * kTabAGranules;
         good = verify_half_fu<true>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace, all_hit, a_ok) &
-               (i < n);
+               act;
       }
     } else {
-      good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
+      good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & act;
     }
 #else
     const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
@@ -789,9 +840,13 @@ __device__ AT2V_INLINE void verify_chunks(
     pace.probe[0] = pace.probe[1] = pace.probe[2] = 0;
 #endif
     uint32_t ticket = 0;
-    if (lane == 0) {
+    if constexpr (kPart) {  // records in list order
+      verdict_or(verdicts, i, good, act, lane);
+    } else if (lane == 0) {
       verdicts[2 * c] = (uint32_t)mask;
       if (2 * c + 1 < nwords) verdicts[2 * c + 1] = (uint32_t)(mask >> 32);
+    }
+    if (lane == 0) {
 #if AT2V_QUEUE
 #if AT2V_SOLO_TAIL
       // the last nwaves/2 chunks go to waves 0..3 only: their SIMD partners leave, so each of those chunks
@@ -832,6 +887,62 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, &c);
+}
+
+// Partitioned cached launches (at2v_cache.h PartArgs): the ladder over the classify kernel's miss list (sender_comb: the
+// comb kernel below takes the hits) or over both lists ([j]A tables: hit chunks skip A's decode and table)
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_miss(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, PartArgs p) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  verify_chunks<false, false, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
+                                    chunk_queue, nullptr, &p);
+}
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_tables_part(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, CacheArgs c,
+    PartArgs p) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  verify_chunks<true, false, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
+                                   chunk_queue, &c, &p);
+}
+
+// The classify kernel of a partitioned cached launch: one record per lane, 64 per wave, in record order. Every sender is
+// looked up exactly as the round-4 kernels did in their chunk prologue (cache_lookup_wave: claims, sightings, epochs),
+// then the wave appends its hits (index, payload, decode verdict) and misses to the two lists with one atomic each.
+__global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c,
+                                                             PartArgs p) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const bool active = i < n;
+  uint32_t Aw[8];
+  load8(Aw, pk + (size_t)(active ? i : n - 1) * 32);
+  const int slot = cache_lookup_wave(c, Aw, lane, active);
+  int a_ok = 0, u = 0;
+  const bool hit = cache_hit(c, slot, Aw, a_ok, u) && active;
+  const uint64_t am = __ballot(active), hm = __ballot(hit), mm = am & ~hm;
+  uint32_t hb = 0, mb = 0;
+  if (lane == 0 && am) {
+    if (hm) hb = atomicAdd(p.counts, (uint32_t)__popcll(hm));
+    if (mm) mb = atomicAdd(p.counts + 1, (uint32_t)__popcll(mm));
+    atomicAdd(c.ctl + kCtlChunks, 1ull);
+    if (hm == am) atomicAdd(c.ctl + kCtlChunkHits, 1ull);
+    if (hm) atomicAdd(c.ctl + kCtlRecHits, (unsigned long long)__popcll(hm));
+  }
+  hb = (uint32_t)__shfl((int)hb, 0);
+  mb = (uint32_t)__shfl((int)mb, 0);
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (hit) {
+    const uint32_t q = hb + (uint32_t)__popcll(hm & below);
+    p.hidx[q] = i;
+    p.hinfo[q] = ((uint32_t)u << 1) | (uint32_t)(a_ok & 1);
+  } else if (active) {
+    p.midx[mb + (uint32_t)__popcll(mm & below)] = i;
+  }
 }
 
 // LDS words of the four-wave split check (in the kernel's `part` array, word-major: [word][lane])
@@ -1175,16 +1286,23 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
 // 127 S + 7 M with two records per lane (~9% of the comb path's multiplications). R'0 and R'1 are parked (X, Y, Z) in the
 // lane's scratch slot while R'2 and R'3 are summed, and reloaded for their encodings. Other chunks run the four quarters
 // through the half-size ladder.
+// kPart: the chunks are 256 entries of the classify kernel's hit list (every record cached), verdict bits set by atomic
+// OR; no ladder branch.
+template <bool kPart = false>
 __device__ AT2V_INLINE void verify_chunks_comb4(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
     uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
-    uint32_t* __restrict__ chunk_queue, const CacheArgs& cc) {
+    uint32_t* __restrict__ chunk_queue, const CacheArgs& cc, const PartArgs* pp = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t nchunks = (n + 255) / 256;
+  uint32_t nchunks = (n + 255) / 256, nh = 0;
+  if constexpr (kPart) {
+    nh = __builtin_amdgcn_readfirstlane(pp->counts[0]);
+    nchunks = (nh + 255) / 256;
+  }
   const int4* __restrict__ comb = cc.payload;
   const uint32_t nwords = (n + 31) / 32;
   int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
@@ -1204,37 +1322,52 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
   for (uint32_t c = c_first; c < nchunks;) {
     const uint32_t i0 = c * 256 + lane;
     int a_ok[4], cidx[4];
-    int hit = 1;
+    uint32_t rec[4];  // the four records of the lane
+    int all_hit;
+    if constexpr (kPart) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {  // every quarter's sender looked up (new keys claimed for the build stream)
-      uint32_t Aw[8];
-      const uint32_t iq = clamp(i0 + 64 * q);
-      load8(Aw, pk + (size_t)iq * 32);
-      hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane, i0 + 64 * q < n), Aw, a_ok[q], cidx[q]) ? 1 : 0;
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t pos = i0 + 64 * q, pc = pos < nh ? pos : nh - 1;
+        rec[q] = pp->hidx[pc];
+        const uint32_t info = pp->hinfo[pc];
+        a_ok[q] = (int)(info & 1u);
+        cidx[q] = (int)(info >> 1);
+      }
+      all_hit = 1;
+    } else {
+      int hit = 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // every quarter's sender looked up (new keys claimed for the build stream)
+        uint32_t Aw[8];
+        rec[q] = clamp(i0 + 64 * q);
+        load8(Aw, pk + (size_t)rec[q] * 32);
+        hit &= cache_hit(cc, cache_lookup_wave(cc, Aw, lane, i0 + 64 * q < n), Aw, a_ok[q], cidx[q]) ? 1 : 0;
+      }
+      all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
+      if (lane == 0) {
+        atomicAdd(cc.ctl + kCtlChunks, 4ull);
+        if (all_hit) atomicAdd(cc.ctl + kCtlChunkHits, 4ull);
+      }
     }
-    const int all_hit = __builtin_amdgcn_readfirstlane(__all(hit) ? 1 : 0);
-    if (lane == 0) {
-      atomicAdd(cc.ctl + kCtlChunks, 4ull);
-      if (all_hit) atomicAdd(cc.ctl + kCtlChunkHits, 4ull);
-    }
+    const uint32_t lim = kPart ? nh : n;  // list / batch positions below lim are real
     int good[4] = {0, 0, 0, 0};
-    if (all_hit) {
+    if (kPart || all_hit) {
       int ok[4];
       fu zz01;
       {
         gu_p3 P0, P1;
-        ok[0] = comb2_point(P0, i0, n, pk, sig, msg, msg_total, off, policy, a_ok[0],
+        ok[0] = comb2_point(P0, rec[0], n, pk, sig, msg, msg_total, off, policy, a_ok[0],
                             comb + (size_t)cidx[0] * (kCombBytes / 16), tbc, sa, sr, lane);
-        ok[1] = comb2_point(P1, i0 + 64, n, pk, sig, msg, msg_total, off, policy, a_ok[1],
+        ok[1] = comb2_point(P1, rec[1], n, pk, sig, msg, msg_total, off, policy, a_ok[1],
                             comb + (size_t)cidx[1] * (kCombBytes / 16), tbc, sa, sr, lane);
         fu_mulc(zz01, P0.Z, P1.Z);
         slot_store(slot, reinterpret_cast<const int32_t*>(&P0), 30);        // X, Y, Z (T not needed)
         slot_store(slot + 8, reinterpret_cast<const int32_t*>(&P1), 30);
       }
       gu_p3 P2, P3;
-      ok[2] = comb2_point(P2, i0 + 128, n, pk, sig, msg, msg_total, off, policy, a_ok[2],
+      ok[2] = comb2_point(P2, rec[2], n, pk, sig, msg, msg_total, off, policy, a_ok[2],
                           comb + (size_t)cidx[2] * (kCombBytes / 16), tbc, sa, sr, lane);
-      ok[3] = comb2_point(P3, i0 + 192, n, pk, sig, msg, msg_total, off, policy, a_ok[3],
+      ok[3] = comb2_point(P3, rec[3], n, pk, sig, msg, msg_total, off, policy, a_ok[3],
                           comb + (size_t)cidx[3] * (kCombBytes / 16), tbc, sa, sr, lane);
       fu zz23, zz, inv, inv01, zi;
       fu_mulc(zz23, P2.Z, P3.Z);
@@ -1243,26 +1376,26 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
       fu_mulc(inv01, inv, zz23);  // 1 / (Z0 Z1)
       fu_mulc(inv, inv, zz01);    // 1 / (Z2 Z3)
       uint32_t Rw[8];
-      load8(Rw, sig + (size_t)clamp(i0 + 128) * 64);
+      load8(Rw, sig + (size_t)rec[2] * 64);
       fu_mulc(zi, inv, P3.Z);
       good[2] = ok[2] & gu_encode_eq_zi(P2, zi, Rw);
-      load8(Rw, sig + (size_t)clamp(i0 + 192) * 64);
+      load8(Rw, sig + (size_t)rec[3] * 64);
       fu_mulc(zi, inv, P2.Z);
       good[3] = ok[3] & gu_encode_eq_zi(P3, zi, Rw);
       gu_p2 Q0, Q1;  // R'0 and R'1 back from the slot
       slot_load(reinterpret_cast<int32_t*>(&Q0), slot, 30);
       slot_load(reinterpret_cast<int32_t*>(&Q1), slot + 8, 30);
-      load8(Rw, sig + (size_t)clamp(i0) * 64);
+      load8(Rw, sig + (size_t)rec[0] * 64);
       fu_mulc(zi, inv01, Q1.Z);
       good[0] = ok[0] & gu_encode_eq_zi(Q0, zi, Rw);
-      load8(Rw, sig + (size_t)clamp(i0 + 64) * 64);
+      load8(Rw, sig + (size_t)rec[1] * 64);
       fu_mulc(zi, inv01, Q0.Z);
       good[1] = ok[1] & gu_encode_eq_zi(Q1, zi, Rw);
     } else {
       // one quarter at a time through ONE inlined copy of the ladder
 #pragma unroll 1
       for (int q = 0; q < 4; ++q) {
-        const uint32_t ii = clamp(i0 + 64 * q);
+        const uint32_t ii = clamp(i0 + 64 * q);  // (not kPart: the hit list never takes this branch)
         uint32_t Rw[8], Sw[8], Aw[8];
         load8(Rw, sig + (size_t)ii * 64);
         load8(Sw, sig + (size_t)ii * 64 + 32);
@@ -1279,11 +1412,15 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint64_t m = __ballot(good[q] & (i0 + 64 * q < n));
-      if (lane == 0) {
-        const uint32_t w0 = 8 * c + 2 * q;
-        if (w0 < nwords) verdicts[w0] = (uint32_t)m;
-        if (w0 + 1 < nwords) verdicts[w0 + 1] = (uint32_t)(m >> 32);
+      if constexpr (kPart) {  // records in list order
+        verdict_or(verdicts, rec[q], good[q], i0 + 64 * q < lim, lane);
+      } else {
+        const uint64_t m = __ballot(good[q] & (i0 + 64 * q < n));
+        if (lane == 0) {
+          const uint32_t w0 = 8 * c + 2 * q;
+          if (w0 < nwords) verdicts[w0] = (uint32_t)m;
+          if (w0 + 1 < nwords) verdicts[w0 + 1] = (uint32_t)(m >> 32);
+        }
       }
     }
     uint32_t ticket = 0;
@@ -1305,13 +1442,26 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
                            // (verify_chunks_comb4); 0: one record per lane
 #endif
 #if AT2V_COMB_PAIRS == 2
-  verify_chunks_comb4(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, c);
+  verify_chunks_comb4<false>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
+                             chunk_queue, c);
 #elif AT2V_COMB_PAIRS
   verify_chunks_comb2(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, c);
 #else
   verify_chunks<true, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
                             chunk_queue, &c);
 #endif
+}
+
+// partitioned cached launches: the classify kernel's hit list by comb additions, four records per lane
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb_part(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, CacheArgs c,
+    PartArgs p) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  verify_chunks_comb4<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
+                            chunk_queue, c, &p);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -2015,9 +2165,12 @@ hipError_t launch_build_btab(int4* out, hipStream_t stream) {
   return hipStreamSynchronize(stream);  // `ident` is a host array of this function's lifetime: wait for the copy
 }
 
+size_t part_bytes_per_record() { return 12; }  // hidx, hinfo, midx
+
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache) {
+                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache,
+                         const PartArgs* part) {
   if (n == 0) return hipSuccess;
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
   if (n <= pair_max && !(cache && cache->comb)) {  // (with combs, small batches take the comb kernel: faster still)
@@ -2038,11 +2191,33 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   // small batches strides over its chunks and needs none (one dependent memset less on the latency path)
   uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesPerBlock);
   const bool lat_comb = cache && cache->comb && n <= pair_max;
-  if (!lat_comb) {
+  const bool parted = cache && part && n > pair_max;  // (zeroes its control words itself, below)
+  if (!lat_comb && !parted) {
     const hipError_t me = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
     if (me != hipSuccess) return me;
   }
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
+  if (cache && part && n > pair_max) {
+    // partitioned (at2v_cache.h PartArgs): classify -> (combs) hit list by comb additions -> ladder over the rest. The
+    // control words after the lane slots: [0] the ladder's chunk queue, [1] the comb kernel's, [4..5] the list sizes.
+    PartArgs pa = *part;
+    pa.counts = queue + 4;
+    hipError_t e = hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cache_classify_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, pk, n, *cache, pa);
+    if (cache->comb) {
+      const uint32_t need2 = ((n + 255) / 256 + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);
+      const int g2 = (int)((uint32_t)grid < need2 ? (uint32_t)grid : need2);
+      hipLaunchKernelGGL(verify_kernel_comb_part, dim3(g2), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n,
+                         policy, verdicts, scratch, btab, queue + 1, *cache, pa);
+      hipLaunchKernelGGL(verify_kernel_miss, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
+                         verdicts, scratch, btab, queue, pa);
+    } else {
+      hipLaunchKernelGGL(verify_kernel_tables_part, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n,
+                         policy, verdicts, scratch, btab, queue, *cache, pa);
+    }
+    return hipGetLastError();
+  }
   if (cache) {  // the kernels look their senders up themselves (at2v_cache.h); builds follow on the build stream
     if (cache->comb && n <= pair_max) {  // small batches: the four-wave split, one block per 64 records
       const uint32_t gl = nchunks < (uint32_t)grid ? nchunks : (uint32_t)grid;

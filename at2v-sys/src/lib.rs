@@ -128,6 +128,7 @@ pub struct At2vInfo {
     pub cache_sightings: u64,
     pub cache_built: u64,
     pub cache_build_us: u64,
+    pub cache_record_hits: u64,
 }
 
 /// `Default`: device 0, DALEK_V1, and the library defaults for every size (65536 records, 1 ms, 256 B, depth 3).

@@ -66,9 +66,10 @@ def parse():
     ap.add_argument("--traffic-leg", type=int, default=1,
                     help="1 = at N=1 also time AT2 traffic (the same records per step, signed by 64 repeating senders) "
                          "through per-sender combs (at2v_opts.sender_comb); reported as at2_traffic, not as value")
-    ap.add_argument("--churn-legs", type=int, default=1,
-                    help="1 = at N=1 also time sender churn through a comb context (distinct keys, Zipf(1.1) over 100k "
-                         "senders, 4x the cache's capacity; fresh records every step): reported as sender_churn")
+    ap.add_argument("--churn-legs", default="distinct,zipf,cap4x",
+                    help="at N=1 also time sender churn through a comb context, these legs (comma list; 0 = none): "
+                         "distinct keys, Zipf(1.1) over 100k senders, 4x the cache's capacity; fresh records every step. "
+                         "Reported as sender_churn")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only (tests): the launcher and gloo control plane with oracle verdicts, no GPU")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
@@ -367,7 +368,7 @@ def main():
             out["multi_gpu"] = multi
     if rank == 0 and world == 1 and args.traffic_leg and not args.senders and not use_dist:
         out["at2_traffic"] = at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L)
-    if rank == 0 and world == 1 and args.churn_legs and not args.senders and not use_dist:
+    if rank == 0 and world == 1 and args.churn_legs not in ("", "0") and not args.senders and not use_dist:
         out["sender_churn"] = churn_legs(args, at2v, torch, dev, lstreams, n, L, kernel_ms, value)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args, d_pk, d_sig, d_msg, n, L)
@@ -433,6 +434,7 @@ def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
             "ms_per_step": dt * 1e3 / steps, "kernel_ms": kernel_ms, "verdicts_ok": ok,
             "cache_chunk_hits": info["cache_chunk_hits"],
             "cache_chunks": info["cache_chunks"],
+            "cache_record_hits": info["cache_record_hits"],
             "roofline": {"bound": "valu", "alg_macs_per_verify": COMB_MAC_PER_VERIFY,
                          "achieved": n * steps / dt * COMB_MAC_PER_VERIFY / 1e12, "peak": MAC_PEAK / 1e12,
                          "unit": "Tops/s (32x32->64 integer MAC, v_mad_u64_u32)",
@@ -470,6 +472,8 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
     }
     out = {}
     for name, keys_of in legs.items():
+        if name not in args.churn_legs.split(","):
+            continue
         v = at2v.BatchVerifier(device=dev.index or 0, policy=args.policy, sender_cache=1024, sender_comb=True)
         batches, key_bufs = [], []
         for b in range(nb):
@@ -512,10 +516,12 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
         kernel_ms = max(ev0.elapsed_time(e) for e in kend) / steps
         ok = all(bool((x == -1).all().item()) for x in vers)
         d = {k: h1[k] - h0[k] for k in ("cache_chunks", "cache_chunk_hits", "cache_claims", "cache_built",
-                                         "cache_build_us", "cache_compactions", "cache_evicted", "cache_sightings")}
+                                         "cache_build_us", "cache_compactions", "cache_evicted", "cache_sightings",
+                                         "cache_record_hits")}
         rate = n * steps / dt
         out[name] = {"value": rate, "unit": "verifies/s", "ms_per_step": dt * 1e3 / steps, "kernel_ms": kernel_ms,
                      "vs_plain": rate / plain_value, "kernel_vs_plain": plain_kernel_ms / kernel_ms,
+                     "record_hit_rate": d["cache_record_hits"] / (n * steps),
                      "chunk_hit_rate": d["cache_chunk_hits"] / max(1, d["cache_chunks"]),
                      "claims_per_step": d["cache_claims"] / steps, "combs_built_per_step": d["cache_built"] / steps,
                      "build_ms_per_step": d["cache_build_us"] / 1e3 / steps,
@@ -528,9 +534,11 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
         torch.cuda.empty_cache()
     out["method"] = ("fresh records every step (GPU generator with a key per record, at2v_gen_records_keys_device), "
                      f"{n} records per step, sender_cache 1024 + sender_comb, two launch streams; wall clock from the "
-                     "first launch to the context's stream drained (builds and compactions included); chunk_hit_rate = "
-                     "chunks (256 records) whose senders were all cached; kernel_ms = device time per step on the "
-                     "launch streams (HIP events)")
+                     "first launch to the context's stream drained (builds and compactions included); record_hit_rate = "
+                     "records verified from their sender's comb (each launch is classified, then the hit list runs "
+                     "the comb kernel and the miss list the ladder); chunk_hit_rate = 64-record groups whose senders "
+                     "were all cached (what round 4's kernels needed); kernel_ms = device time per step on the launch "
+                     "streams (HIP events)")
     return out
 
 

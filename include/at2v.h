@@ -27,7 +27,8 @@ extern "C" {
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
  * version 6 appended at2v_opts.cpu_threads / flags (num_gpus = 0 now means the CPU batch backend, no device),
- * at2v_info.cpu_threads / cpu_batches / cpu_fallbacks / cache_sightings / cache_built / cache_build_us,
+ * at2v_info.cpu_threads / cpu_batches / cpu_fallbacks / cache_sightings / cache_built / cache_build_us /
+ * cache_record_hits,
  * at2v_gen_records_keys_device, at2v_queue_opts.cpu_threads (with the
  * AT2V_QUEUE_CPU / AT2V_QUEUE_CPU_FALLBACK flags) and at2v_queue_stats.cpu_fallbacks; version 5 appended at2v_queue_opts.sender_cache and at2v_info.cache_capacity / cache_claims / cache_evicted /
  * cache_compactions (the sender cache replaces entries instead of restarting empty); version 4 appended
@@ -189,6 +190,8 @@ typedef struct {
   uint64_t cache_sightings;  /* first sightings recorded instead of claiming a payload (admission, AT2V_CTX_ADMIT_FIRST) */
   uint64_t cache_built;      /* payloads (tables or combs) built */
   uint64_t cache_build_us;   /* device time of the build passes that built something (first build block to the flip) */
+  uint64_t cache_record_hits;/* records whose sender came from the cache (launches above small_batch_max verify each
+                                record by its own sender's entry, whatever the other records of its chunk) */
 } at2v_info;
 /* With a sender cache, at2v_get_info first waits for the context's cache work (its build stream, which follows every
  * cached launch and therefore waits for those launches, and whatever each launch's stream ran before them). */

@@ -451,3 +451,49 @@ def test_compaction_while_launches_overlap_on_two_streams(at2v_mod, oracle, comb
         info = v.info()
     print("two-stream compactions:", info)
     assert info["cache_compactions"] >= 2 and info["cache_entries"] <= 16, info
+
+
+def test_partitioned_mixed_traffic_record_hits(at2v_mod, oracle, comb):
+    """Round 5's partitioned launch: records of 64 cached senders shuffled with records of fresh keys (adversarial set),
+    so no 64- or 256-record chunk is all-cached. The classify kernel sends every record of a cached sender down the
+    cached path anyway (hit list: comb additions, or [j]A tables) and the rest down the ladder; verdicts equal the
+    oracle's, and the cached-record count equals the number of records signed by the 64 senders."""
+    pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
+    p1, s1, m1 = _mutate(pk, sig, msg, off, np.random.default_rng(53), 150, kinds=3)
+    pa, sa, ma, oa, cls = oracle.gen_adversarial(CFG_SEED + 57, 0, 4096, 48)
+    P = np.concatenate([p1, pa])
+    S = np.concatenate([s1, sa])
+    msgs = [m1[off[i]:off[i + 1]] for i in range(len(p1))] + [ma[oa[i]:oa[i + 1]] for i in range(len(pa))]
+    perm = np.random.default_rng(59).permutation(len(P))
+    P, S = P[perm], S[perm]
+    msgs = [msgs[i] for i in perm]
+    M = np.concatenate(msgs)
+    O = np.concatenate([[0], np.cumsum([len(m) for m in msgs])]).astype(np.uint32)
+    want = oracle.verify_batch(P, S, M, O)
+    assert 0 < want.sum() < len(want)
+    cfg1_keys = {bytes(r) for r in pk[:64]}
+    n_cfg1 = sum(bytes(r) in cfg1_keys for r in P)
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1 << 14, sender_comb=comb, admit_first=True) as v:
+        assert np.array_equal(v.verify_batch(pk, sig, msg, off), oracle.verify_batch(pk, sig, msg, off))
+        h0 = v.info()  # (waits for the 64 senders' entries)
+        got = v.verify_batch(P, S, M, O)
+        assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+        h1 = v.info()
+        hits = h1["cache_record_hits"] - h0["cache_record_hits"]
+        assert hits >= n_cfg1, (hits, n_cfg1)
+        assert h1["cache_chunk_hits"] - h0["cache_chunk_hits"] < (h1["cache_chunks"] - h0["cache_chunks"]) // 4
+        for _ in range(2):  # the adversarial keys are cached now too (admit_first): more hits, same verdicts
+            assert np.array_equal(v.verify_batch(P, S, M, O), want)
+        assert v.info()["cache_record_hits"] - h1["cache_record_hits"] > 2 * hits
+
+
+@pytest.mark.parametrize("partition", ["0", "1"])
+def test_partition_switch_same_verdicts(at2v_mod, golden, monkeypatch, comb, partition):
+    """AT2V_CACHE_PARTITION=0 keeps round 4's in-kernel lookup for launches above small_batch_max (A/B switch): both
+    forms give the golden verdicts, cold and warm"""
+    monkeypatch.setenv("AT2V_CACHE_PARTITION", partition)
+    g = golden["adversarial"]
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=4096, sender_comb=comb) as v:
+        for rep in range(3):
+            assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek), rep
+            v.info()

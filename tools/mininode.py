@@ -226,6 +226,25 @@ def client_main(inboxes, ready_q, args):
     ready_q.put({"offered_s": time.perf_counter() - t_start})
 
 
+def polluter_main(ready, stop):
+    """--polluter: another process on the same GPU that holds what a test runner or a co-located job holds: an RCCL
+    communicator (libat2v's, world 1), torch streams and two raw HIP streams, each used once, idle afterwards. Its
+    hardware queues stay mapped for the whole run (DESIGN.md §10e "Hardware queues")."""
+    import torch
+
+    import at2v
+    v = at2v.BatchVerifier(device=0)
+    v.comm_init_rank(at2v.comm_unique_id(), 0, 1)
+    streams = [torch.cuda.Stream() for _ in range(4)] + at2v.launch_streams(2)
+    for st in streams:
+        with torch.cuda.stream(st):
+            torch.ones(1024, device="cuda").sum().item()
+    torch.cuda.synchronize()
+    ready.set()
+    stop.wait(900)
+    v.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=4)
@@ -244,8 +263,17 @@ def main():
                     help="amounts in [1, max]; small enough that no sender can underflow, so the final ledger does "
                          "not depend on each node's delivery order (the reference bumps the sequence on Underflow)")
     ap.add_argument("--seed", type=int, default=0x4154325F)
+    ap.add_argument("--polluter", type=int, default=0,
+                    help="1 = a separate process holds an RCCL communicator and 6 streams on the GPU for the whole run")
     args = ap.parse_args()
     ctx = mp.get_context("spawn")
+    pol = None
+    if args.polluter:
+        pol_ready, pol_stop = ctx.Event(), ctx.Event()
+        pol = ctx.Process(target=polluter_main, args=(pol_ready, pol_stop))
+        pol.start()
+        if not pol_ready.wait(300):
+            raise SystemExit("mininode: the polluter process did not come up")
     inboxes = [ctx.Queue() for _ in range(args.nodes)]
     ready_q, result_q = ctx.Queue(), ctx.Queue()
     cl = ctx.Process(target=client_main, args=(inboxes, ready_q, args))
@@ -280,6 +308,11 @@ def main():
            "bad_signatures": info["bad"], "fresh_senders": info["fresh"], "batch_B": args.batch, "delay_us": args.delay_us,
            "p50_us": max(r["lat_p50_us"] for r in res), "p99_us": max(r["lat_p99_us"] for r in res),
            "ledgers_identical": same, "all_real_applied": all(r["applied"] == info["total"] - info["bad"] for r in res), "wall_s": wall, "offered_s": offered["offered_s"], "per_node": res}
+    out["polluter"] = bool(args.polluter)
+    out["queue_env"] = {k: v for k, v in os.environ.items() if k.startswith("AT2V_QUEUE")}
+    if pol is not None:
+        pol_stop.set()
+        pol.join(timeout=60)
     print(json.dumps(out), flush=True)
     ok = same and all(r["verified"] + r["rejected"] == info["total"] and r["rejected"] == info["bad"] and
                       r["applied"] == info["total"] - info["bad"] and r["pending"] == 0 and r["failed"] == 0 for r in res)
