@@ -243,16 +243,18 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit
   for (int t = 0; t < 2; ++t) {
     AT2V_TRY(c->tags[t].ensure((size_t)cap * 8));
     AT2V_TRY(c->entries[t].ensure((size_t)cap * at2v::cache_entry_bytes()));
-    AT2V_TRY(hipMemset(c->tags[t].p, 0, c->tags[t].cap));
-    AT2V_TRY(hipMemset(c->entries[t].p, 0, c->entries[t].cap));  // every entry invalid
+    // (on the shard's stream, as every other operation of a context: a process that never touches the null stream maps
+    // one hardware queue less)
+    AT2V_TRY(hipMemsetAsync(c->tags[t].p, 0, c->tags[t].cap, s.stream));
+    AT2V_TRY(hipMemsetAsync(c->entries[t].p, 0, c->entries[t].cap, s.stream));  // every entry invalid
   }
   AT2V_TRY(c->payload.ensure((size_t)capacity * at2v::cache_payload_bytes(a.comb)));
   AT2V_TRY(c->free_slots.ensure((size_t)capacity * 4));
   AT2V_TRY(c->used.ensure((size_t)capacity * 4));
   AT2V_TRY(c->ctl.ensure(ctl_bytes));
-  AT2V_TRY(hipMemset(c->ctl.p, 0, c->ctl.cap));
+  AT2V_TRY(hipMemsetAsync(c->ctl.p, 0, c->ctl.cap, s.stream));
   AT2V_TRY(c->seen.ensure(((size_t)a.seen_mask + 1) * 8));
-  AT2V_TRY(hipMemset(c->seen.p, 0, c->seen.cap));
+  AT2V_TRY(hipMemsetAsync(c->seen.p, 0, c->seen.cap, s.stream));
   for (int j = 0; j < kClaimSlots; ++j) AT2V_TRY(c->claim_list[j].ensure((size_t)capacity * 16));
   a.tags = (unsigned long long*)c->tags[0].p;
   a.entries = (int4*)c->entries[0].p;
@@ -956,7 +958,8 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(sh.device) == hipSuccess && hipStreamSynchronize(sh.cache->build) == hipSuccess &&
-        hipMemcpy(w.data(), sh.cache->ctl.p, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+        hipMemcpyAsync(w.data(), sh.cache->ctl.p, w.size() * 8, hipMemcpyDeviceToHost, sh.cache->build) == hipSuccess &&
+        hipStreamSynchronize(sh.cache->build) == hipSuccess) {
       const uint64_t fc = w[at2v::kCtlFreeCount], fh = w[at2v::kCtlFreeHead];
       const uint64_t cap = sh.cache->args.capacity;
       out->cache_entries += (cap - std::min(fc, cap)) + std::min(fh, fc);  // keys holding a payload

@@ -73,9 +73,13 @@ struct HipBackend {
   // (one host-to-device copy and its cross-stream wait less on the latency path; config 5 queue p50 123-130 -> 109-117
   // us, p99 242-285 -> 154-187 us, profiles/r04w). AT2V_QUEUE_ZEROCOPY overrides (0 = always upload).
   uint32_t zerocopy_max = 1024;
-  // Compute streams the queue alternates over (AT2V_QUEUE_STREAMS, 1 or 2) and their priority (AT2V_QUEUE_PRIORITY = 1:
-  // the device's greatest stream priority). The host-to-device stream is created on the first batch that needs an
-  // upload (above zerocopy_max records), so a latency-mode node maps fewer hardware queues.
+  // Compute streams the queue alternates over: 2 in throughput mode (batch k+1's kernel fills the CUs batch k's leaves),
+  // 1 in latency mode (AT2V_QUEUE_EAGER: batches are small and rarely overlap). AT2V_QUEUE_STREAMS overrides (1 or 2),
+  // AT2V_QUEUE_PRIORITY = 1 gives them the device's greatest stream priority (A/B). The host-to-device stream is
+  // created on the first batch that needs an upload (above zerocopy_max records). A latency-mode node so maps two
+  // hardware queues (its stream and the context's), not four: with another process holding an RCCL communicator and six
+  // streams on the same GPU, config-5 p99 was 0.70-0.97 ms per node with four and 0.56 ms with two, as without that
+  // process (0.54-0.56 ms); priority changed nothing (profiles/r05f).
   int ncomp = 2;
   bool prio = false;
 
@@ -101,6 +105,7 @@ struct HipBackend {
     if (const char* v = std::getenv("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
     if (const char* v = std::getenv("AT2V_QUEUE_ZEROCOPY")) zerocopy_max = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
+    if (o.flags & AT2V_QUEUE_EAGER) ncomp = 1;
     if (const char* v = std::getenv("AT2V_QUEUE_STREAMS")) ncomp = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("AT2V_QUEUE_PRIORITY")) prio = std::atoi(v) != 0;
     const DeviceScope scope(device);

@@ -514,7 +514,13 @@ __device__ AT2V_INLINE uint64_t cache_fingerprint(const uint32_t a[8], uint64_t 
 // the entry's key and meta {0, valid 0, u, epoch}; claims that got a payload are appended to the launch's claim set for
 // the build stream. A claim that finds the free list empty (u = -1) or a record whose probe path is full flags the cache
 // full (compaction before the next launch). Returns the entry slot or -1.
-__device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t a[8], int lane, bool active = true) {
+// statistics of a caller that sums its lookups itself (wave-uniform), instead of one atomic per counter per wave
+struct LookupStats {
+  uint32_t found = 0, claimed = 0, failed = 0, sighted = 0;
+};
+
+__device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t a[8], int lane, bool active = true,
+                                             LookupStats* st = nullptr) {
   const uint32_t mask = c.cap - 1;
   int slot = -1, claimed = 0, found = 0, want = 0;
   uint64_t fp = cache_fingerprint(a, c.seed, c.fp_mask);
@@ -608,13 +614,23 @@ __device__ AT2V_INLINE int cache_lookup_wave(const CacheArgs& c, const uint32_t 
   // (a tail lane past n is no failure either: it must not flag the cache full)
   const uint64_t fm = __ballot(found), xm = __ballot(slot < 0 && !deferred && active), sgm = __ballot(sighted);
   unsigned long long nbase = 0;
+  if (st) {
+    st->found += (uint32_t)__popcll(fm);
+    st->claimed += (uint32_t)__popcll(cm);
+    st->failed += (uint32_t)__popcll(xm);
+    st->sighted += (uint32_t)__popcll(sgm);
+  }
   if (lane == 0) {
     if (pm) nbase = atomicAdd(c.ctl + c.count_word, (unsigned long long)__popcll(pm));
-    if (cm) atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
-    if (fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
-    if (xm) atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
-    if (sgm) atomicAdd(c.ctl + kCtlSighted, (unsigned long long)__popcll(sgm));
-    if (cm != pm || xm) atomicExch(c.ctl + kCtlFull, 1ull);
+    if (!st) {
+      if (cm) atomicAdd(c.ctl + kCtlClaimed, (unsigned long long)__popcll(cm));
+      if (fm) atomicAdd(c.ctl + kCtlFound, (unsigned long long)__popcll(fm));
+      if (xm) atomicAdd(c.ctl + kCtlFailed, (unsigned long long)__popcll(xm));
+      if (sgm) atomicAdd(c.ctl + kCtlSighted, (unsigned long long)__popcll(sgm));
+    }
+    // (a plain load first: a full cache under churn would otherwise have every wave exchange the same word)
+    if ((cm != pm || xm) && __hip_atomic_load(c.ctl + kCtlFull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      atomicExch(c.ctl + kCtlFull, 1ull);
   }
   nbase = __shfl(nbase, 0);
   if (claimed) {
@@ -911,37 +927,85 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
                                    chunk_queue, &c, &p);
 }
 
-// The classify kernel of a partitioned cached launch: one record per lane, 64 per wave, in record order. Every sender is
-// looked up exactly as the round-4 kernels did in their chunk prologue (cache_lookup_wave: claims, sightings, epochs),
-// then the wave appends its hits (index, payload, decode verdict) and misses to the two lists with one atomic each.
+// The classify kernel of a partitioned cached launch: one record per lane, a wave takes kClassifyGroups consecutive
+// 64-record groups. Every sender is looked up exactly as the round-4 kernels did in their chunk prologue
+// (cache_lookup_wave: claims, sightings, epochs); the wave then takes room in the two lists with one atomic per list and
+// writes its hits (index, payload, decode verdict) and misses in group order, and the block adds its statistics with
+// one atomic per counter. (One wave per group with per-wave atomics took 0.54-0.77 ms per 1M records: ~100k atomics on
+// a handful of control words, profiles/r05f.)
+constexpr int kClassifyGroups = 8;
 __global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c,
                                                              PartArgs p) {
+  __shared__ uint32_t sstat[4][8];
   const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  const bool active = i < n;
-  uint32_t Aw[8];
-  load8(Aw, pk + (size_t)(active ? i : n - 1) * 32);
-  const int slot = cache_lookup_wave(c, Aw, lane, active);
-  int a_ok = 0, u = 0;
-  const bool hit = cache_hit(c, slot, Aw, a_ok, u) && active;
-  const uint64_t am = __ballot(active), hm = __ballot(hit), mm = am & ~hm;
+  const int wib = threadIdx.x >> 6;
+  const uint32_t ngroups = (n + 63) / 64;
+  const uint32_t g0 = (blockIdx.x * 4 + (uint32_t)wib) * kClassifyGroups;
+  LookupStats st;
+  uint64_t hm[kClassifyGroups], am[kClassifyGroups];
+  uint32_t info[kClassifyGroups];
+  uint32_t nh = 0, na = 0, chunks = 0, chunk_hits = 0;
+#pragma unroll
+  for (int g = 0; g < kClassifyGroups; ++g) {
+    hm[g] = am[g] = 0;
+    info[g] = 0;
+    if (g0 + g < ngroups) {  // wave-uniform
+      const uint32_t i = (g0 + g) * 64 + lane;
+      const bool active = i < n;
+      uint32_t Aw[8];
+      load8(Aw, pk + (size_t)(active ? i : n - 1) * 32);
+      const int slot = cache_lookup_wave(c, Aw, lane, active, &st);
+      int a_ok = 0, u = 0;
+      const bool hit = cache_hit(c, slot, Aw, a_ok, u) && active;
+      am[g] = __ballot(active);
+      hm[g] = __ballot(hit);
+      info[g] = ((uint32_t)u << 1) | (uint32_t)(a_ok & 1);
+      nh += (uint32_t)__popcll(hm[g]);
+      na += (uint32_t)__popcll(am[g]);
+      ++chunks;
+      chunk_hits += hm[g] == am[g] ? 1u : 0u;
+    }
+  }
+  const uint32_t nm = na - nh;
   uint32_t hb = 0, mb = 0;
-  if (lane == 0 && am) {
-    if (hm) hb = atomicAdd(p.counts, (uint32_t)__popcll(hm));
-    if (mm) mb = atomicAdd(p.counts + 1, (uint32_t)__popcll(mm));
-    atomicAdd(c.ctl + kCtlChunks, 1ull);
-    if (hm == am) atomicAdd(c.ctl + kCtlChunkHits, 1ull);
-    if (hm) atomicAdd(c.ctl + kCtlRecHits, (unsigned long long)__popcll(hm));
+  if (lane == 0) {
+    if (nh) hb = atomicAdd(p.counts, nh);
+    if (nm) mb = atomicAdd(p.counts + 1, nm);
   }
   hb = (uint32_t)__shfl((int)hb, 0);
   mb = (uint32_t)__shfl((int)mb, 0);
   const uint64_t below = (1ull << lane) - 1ull;
-  if (hit) {
-    const uint32_t q = hb + (uint32_t)__popcll(hm & below);
-    p.hidx[q] = i;
-    p.hinfo[q] = ((uint32_t)u << 1) | (uint32_t)(a_ok & 1);
-  } else if (active) {
-    p.midx[mb + (uint32_t)__popcll(mm & below)] = i;
+#pragma unroll
+  for (int g = 0; g < kClassifyGroups; ++g) {
+    const uint32_t i = (g0 + g) * 64 + lane;
+    const uint64_t mm = am[g] & ~hm[g];
+    if ((hm[g] >> lane) & 1ull) {
+      const uint32_t q = hb + (uint32_t)__popcll(hm[g] & below);
+      p.hidx[q] = i;
+      p.hinfo[q] = info[g];
+    } else if ((mm >> lane) & 1ull) {
+      p.midx[mb + (uint32_t)__popcll(mm & below)] = i;
+    }
+    hb += (uint32_t)__popcll(hm[g]);
+    mb += (uint32_t)__popcll(mm);
+  }
+  if (lane == 0) {
+    sstat[wib][0] = chunks;
+    sstat[wib][1] = chunk_hits;
+    sstat[wib][2] = nh;
+    sstat[wib][3] = st.found;
+    sstat[wib][4] = st.claimed;
+    sstat[wib][5] = st.failed;
+    sstat[wib][6] = st.sighted;
+    sstat[wib][7] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 7) {
+    const uint32_t v = sstat[0][threadIdx.x] + sstat[1][threadIdx.x] + sstat[2][threadIdx.x] + sstat[3][threadIdx.x];
+    const int k = threadIdx.x;
+    const int word = k == 0 ? kCtlChunks : k == 1 ? kCtlChunkHits : k == 2 ? kCtlRecHits : k == 3 ? kCtlFound
+                     : k == 4 ? kCtlClaimed : k == 5 ? kCtlFailed : kCtlSighted;
+    if (v) atomicAdd(c.ctl + word, (unsigned long long)v);
   }
 }
 
@@ -2204,7 +2268,9 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
     pa.counts = queue + 4;
     hipError_t e = hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(cache_classify_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, pk, n, *cache, pa);
+    const uint32_t groups = (n + 63) / 64, per_block = 4 * kClassifyGroups;
+    hipLaunchKernelGGL(cache_classify_kernel, dim3((groups + per_block - 1) / per_block), dim3(256), 0, stream, pk, n,
+                       *cache, pa);
     if (cache->comb) {
       const uint32_t need2 = ((n + 255) / 256 + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);
       const int g2 = (int)((uint32_t)grid < need2 ? (uint32_t)grid : need2);

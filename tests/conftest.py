@@ -17,16 +17,8 @@ for p in (ROOT, os.path.join(ROOT, "at2-node_amd"), os.path.join(ROOT, "tests"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (parity tests through the C ABI)")
-    config.addinivalue_line("markers", "clean_gpu: multi-process latency test; runs before every other test, while the "
-                            "pytest process itself holds no GPU queues")
-
-
-def pytest_collection_modifyitems(session, config, items):
-    """Config-5 latency tests run 4 node processes + a client on one GPU. Once the pytest process has used RCCL and
-    several streams, its idle hardware queues stay mapped and the nodes' p99 rises from 0.33-0.68 ms to 0.8-1.5 ms
-    (gpurun_out/r04n: probe1 alone vs probe2 after the RCCL tests, profiles/r04n). A node process owns its GPU in
-    deployment, so these tests run first."""
-    items.sort(key=lambda it: 0 if it.get_closest_marker("clean_gpu") else 1)  # stable: file order otherwise
+    config.addinivalue_line("markers", "clean_gpu: multi-process latency test (no ordering: since round 5 a latency-mode "
+                            "queue maps two hardware queues, and its p99 holds with other GPU processes around)")
 
 
 @pytest.fixture(scope="session")

@@ -264,16 +264,21 @@ def main():
                          "not depend on each node's delivery order (the reference bumps the sequence on Underflow)")
     ap.add_argument("--seed", type=int, default=0x4154325F)
     ap.add_argument("--polluter", type=int, default=0,
-                    help="1 = a separate process holds an RCCL communicator and 6 streams on the GPU for the whole run")
+                    help="N > 0 = N separate processes each hold an RCCL communicator and 6 streams on the GPU for the "
+                         "whole run")
+    ap.add_argument("--node-hw-queues", type=int, default=0,
+                    help="K > 0 = the node processes run with GPU_MAX_HW_QUEUES=K (HIP's hardware queues per process)")
     args = ap.parse_args()
     ctx = mp.get_context("spawn")
-    pol = None
-    if args.polluter:
-        pol_ready, pol_stop = ctx.Event(), ctx.Event()
+    pols = []
+    pol_stop = ctx.Event()
+    for _ in range(args.polluter):
+        pol_ready = ctx.Event()
         pol = ctx.Process(target=polluter_main, args=(pol_ready, pol_stop))
         pol.start()
+        pols.append(pol)
         if not pol_ready.wait(300):
-            raise SystemExit("mininode: the polluter process did not come up")
+            raise SystemExit("mininode: a polluter process did not come up")
     inboxes = [ctx.Queue() for _ in range(args.nodes)]
     ready_q, result_q = ctx.Queue(), ctx.Queue()
     cl = ctx.Process(target=client_main, args=(inboxes, ready_q, args))
@@ -290,8 +295,16 @@ def main():
     KEYS[:] = info["keys"]
     nodes = [ctx.Process(target=node_main_with_keys, args=(i, inboxes, result_q, args, info["keys"], info["total"]))
              for i in range(args.nodes)]
+    saved = os.environ.get("GPU_MAX_HW_QUEUES")
+    if args.node_hw_queues > 0:  # (spawned children take the parent's environment at start)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.node_hw_queues)
     for p in nodes:
         p.start()
+    if args.node_hw_queues > 0:
+        if saved is None:
+            del os.environ["GPU_MAX_HW_QUEUES"]
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = saved
     time.sleep(3.0)  # contexts up (first HIP init per process)
     t0 = time.perf_counter()
     ready_q.put("go")
@@ -308,10 +321,11 @@ def main():
            "bad_signatures": info["bad"], "fresh_senders": info["fresh"], "batch_B": args.batch, "delay_us": args.delay_us,
            "p50_us": max(r["lat_p50_us"] for r in res), "p99_us": max(r["lat_p99_us"] for r in res),
            "ledgers_identical": same, "all_real_applied": all(r["applied"] == info["total"] - info["bad"] for r in res), "wall_s": wall, "offered_s": offered["offered_s"], "per_node": res}
-    out["polluter"] = bool(args.polluter)
+    out["polluters"] = args.polluter
+    out["node_hw_queues"] = args.node_hw_queues or None
     out["queue_env"] = {k: v for k, v in os.environ.items() if k.startswith("AT2V_QUEUE")}
-    if pol is not None:
-        pol_stop.set()
+    pol_stop.set()
+    for pol in pols:
         pol.join(timeout=60)
     print(json.dumps(out), flush=True)
     ok = same and all(r["verified"] + r["rejected"] == info["total"] and r["rejected"] == info["bad"] and

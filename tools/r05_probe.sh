@@ -5,6 +5,9 @@
 #   distprof   rocprofv3 kernel trace of the headline + the distinct-key churn leg (verify_kernel vs the partitioned
 #              launch's classify and miss kernels on the same kind of records)
 #   partab     the same traffic, wall-clock rate with AT2V_CACHE_PARTITION=0 / 1 alternating (2 rounds)
+#   pollute2   config 5 (2% first-seen) beside TWO polluter processes, node processes with HIP's default 4 hardware
+#              queues vs GPU_MAX_HW_QUEUES=2 (2 rounds)
+#   stallat2   tools/stall_pmc_at2.sh (wave-cycle split of the comb kernel on AT2 traffic)
 #   pollute    config 5 with 2% first-seen senders, without / with a polluter process (RCCL + 6 streams), for the queue
 #              stream settings default / AT2V_QUEUE_STREAMS=1 / AT2V_QUEUE_STREAMS=1 + AT2V_QUEUE_PRIORITY=1
 set -o pipefail
@@ -36,6 +39,12 @@ for st in "$@"; do
                    --delay-us 1000 --eager 1 --comb 1 --fresh-frac 0.02 --polluter $p
                done
              done ;;
+    pollute2) for r in 1 2; do for mode in default hwq2; do
+                case $mode in default) E="";; hwq2) E="--node-hw-queues 2";; esac
+                run c5_pol2_${mode}_$r 240 python3 tools/mininode.py --nodes 4 --rate 20000 --seconds 2 --batch 1024 \
+                  --delay-us 1000 --eager 1 --comb 1 --fresh-frac 0.02 --polluter 2 $E
+              done; done ;;
+    stallat2) run stallat2 400 bash tools/stall_pmc_at2.sh $TAG ;;
     *) echo "[probe] unknown stage $st"; exit 2 ;;
   esac
 done
