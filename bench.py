@@ -456,7 +456,7 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
       zipf      keys Zipf(1.1) over 100,000 senders (a few heavy senders, a long tail of one-shot ones);
       cap4x     keys uniform over 4,096 senders, 4x the cache's capacity (continuous replacement).
     A key claims its comb at its second sighting (admission), combs are built on the context's stream, compactions
-    run there too; the timed region ends after that stream has drained (v.info()), so builds and compactions are
+    run there too; at most two batches are in flight (a node's queue of depth 3); the timed region ends after that stream has drained (v.info()), so builds and compactions are
     charged to the leg. Per leg: wall-clock rate, device time of the launch streams, chunk hit rate, claims, builds
     and their device time, compactions, sightings; vs_plain = this leg's rate over the headline's (distinct keys,
     no cache)."""
@@ -508,6 +508,8 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
         ev0.record(lstreams[0])
         lstreams[1].wait_event(ev0)
         for k in range(steps):
+            if k >= 2:  # at most two batches in flight, as a node's ingest queue (depth 3) has: the host keeps up with
+                kend[k - 2].synchronize()  # the cache counters, so compactions and claims happen between batches
             step(warm + k)
             kend[k].record(lstreams[k % 2])
         torch.cuda.synchronize(dev)
