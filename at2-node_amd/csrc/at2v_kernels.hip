@@ -325,14 +325,50 @@ struct DevTabB {
   }
 };
 
+// Per-wait probe of the comb kernel (a variant build: tools/build_variant.sh <tag> -DAT2V_COMB_PROBE, read by
+// tools/ab_bench.py --probe through at2v_probe_read): s_memtime cycles per wave in each wait and phase of
+// verify_chunks_comb4, summed over the launch. Product builds: just stmt.
+#if defined(AT2V_COMB_PROBE) && defined(__HIP_DEVICE_COMPILE__)
+#define AT2V_CPROBE(acc, stmt)                                  \
+  do {                                                          \
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime(); \
+    stmt;                                                       \
+    (acc) += __builtin_amdgcn_s_memtime() - t0_;                \
+  } while (0)
+#else
+#define AT2V_CPROBE(acc, stmt) stmt
+#endif
+#ifdef AT2V_COMB_PROBE
+enum {
+  kCpAWait,     // A-comb entry: vmcnt wait before the stage is read
+  kCpBWait,     // B-comb entry: the same
+  kCpStage,     // lgkmcnt wait before a stage is refilled
+  kCpRecord,    // the record's R, S, A, offsets loaded + the prechecks
+  kCpSha,       // SHA-512(R || A || M) mod l, recodes (message loads included)
+  kCpSums,      // the 26 A + 16 B comb additions (the three waits above included)
+  kCpFinish,    // slot round trip, shared inversion, four encodes + compares
+  kCpBook,      // list loads, verdict ORs, chunk ticket
+  kCpChunk,     // chunk total
+  kCpChunks,    // chunks (count)
+  kCpN
+};
+__device__ unsigned long long at2v_cprobe_acc[kCpN];
+struct CombProbe {
+  unsigned long long v[kCpN] = {};
+};
+#endif
+
 // Comb entries (at2v_comb.h) by LDS-DMA into two alternating per-wave stages: the entry of the next addition lands while
 // this one is computed. TabC: C[i][j] of this lane's key (CombEntry, kCombGranules); TabBC: D[i][j] (affine Niels, 8).
 struct DevComb {
   const int4* base;  // this lane's key's comb
   int4* stage[2];    // this wave's two 10 KiB stages (wave-uniform)
   int lane;
+#ifdef AT2V_COMB_PROBE
+  mutable unsigned long long waited = 0, stage_waited = 0;
+#endif
   __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's previous entry has been read out
+    AT2V_CPROBE(stage_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));  // the stage's previous entry is read
 #if AT2V_EXP_COMB_HOT  // EXPERIMENT (wrong verdicts, timing only): every A entry read is the same cache-hot line
     i = 0;
     j = 1;
@@ -345,7 +381,7 @@ struct DevComb {
   }
   __device__ AT2V_INLINE void load_prefetched(int st, CombEntry& c) const {
     static_assert(sizeof(CombEntry) <= (size_t)kCombWords * 4, "comb entry words");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AT2V_CPROBE(waited, asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
     int32_t w[kCombWords];
 #pragma unroll
     for (int q = 0; q < kCombGranules; ++q) {
@@ -364,8 +400,11 @@ struct DevBComb {
   const int4* base;  // the context's comb of B
   int4* stage[2];
   int lane;
+#ifdef AT2V_COMB_PROBE
+  mutable unsigned long long waited = 0, stage_waited = 0;
+#endif
   __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    AT2V_CPROBE(stage_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));
 #if AT2V_EXP_COMB_HOT
     i = 0;
     j = 1;
@@ -379,7 +418,7 @@ struct DevBComb {
   template <class Niels>
   __device__ AT2V_INLINE void load_prefetched(int st, Niels& n) const {
     static_assert(sizeof(Niels) == 120, "Niels point: 30 words");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AT2V_CPROBE(waited, asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
     int32_t w[32];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -1230,19 +1269,54 @@ __device__ AT2V_INLINE int comb2_point(gu_p3& P, uint32_t i, uint32_t n, const u
                                        const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                        uint32_t msg_total, const uint32_t* __restrict__ off, int policy, int a_ok,
                                        const int4* __restrict__ comb_key, const DevBComb& tbc, int4* sa, int4* sr,
-                                       int lane) {
+                                       int lane
+#ifdef AT2V_COMB_PROBE
+                                       , CombProbe* pr = nullptr
+#endif
+) {
   const uint32_t ii = i < n ? i : n - 1;
   uint32_t Rw[8], Sw[8], Aw[8];
-  load8(Rw, sig + (size_t)ii * 64);
-  load8(Sw, sig + (size_t)ii * 64 + 32);
-  load8(Aw, pk + (size_t)ii * 32);
-  const uint32_t o0 = off[ii], len = off[ii + 1] - o0;
-  const int ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
+  int ok;
+  uint32_t o0, len;
+#ifdef AT2V_COMB_PROBE
+  unsigned long long dummy = 0;
+  unsigned long long& p_rec = pr ? pr->v[kCpRecord] : dummy;
+  (void)p_rec;
+#endif
+  AT2V_CPROBE(p_rec, {
+    load8(Rw, sig + (size_t)ii * 64);
+    load8(Sw, sig + (size_t)ii * 64 + 32);
+    load8(Aw, pk + (size_t)ii * 32);
+    o0 = off[ii];
+    len = off[ii + 1] - o0;
+    ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
+  });
   const DevComb tc{comb_key, {sa, sr}, lane};
   with_msg_reader(msg, msg_total, o0, len, [&](auto& mwd) {
+#ifdef AT2V_COMB_PROBE
+    if (pr) {  // comb_point with its two phases timed apart
+      uint32_t kd[kCombDigitWords], sd[8];
+      AT2V_CPROBE(pr->v[kCpSha], {
+        comb_k_digits(kd, Rw, Aw, len, mwd);
+        sc_recode16(sd, Sw);
+      });
+      AT2V_CPROBE(pr->v[kCpSums], {
+        gu_p3_identity(P);
+        comb_sum<true>(P, kd, 0, kCombPos, tc);
+        comb_sum<false>(P, sd, 0, kBCombPos, tbc);
+      });
+      return 0;
+    }
+#endif
     comb_point(P, Rw, Aw, Sw, len, mwd, tc, tbc);
     return 0;
   });
+#ifdef AT2V_COMB_PROBE
+  if (pr) {
+    pr->v[kCpAWait] += tc.waited;
+    pr->v[kCpStage] += tc.stage_waited;
+  }
+#endif
   return ok;
 }
 
@@ -1383,7 +1457,17 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
                                             : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
   auto clamp = [n](uint32_t i) { return i < n ? i : n - 1; };
+#ifdef AT2V_COMB_PROBE
+  CombProbe probe;
+  CombProbe* const pr = kPart ? &probe : nullptr;
+#define AT2V_CP_ARG , pr
+#else
+#define AT2V_CP_ARG
+#endif
   for (uint32_t c = c_first; c < nchunks;) {
+#ifdef AT2V_COMB_PROBE
+    const unsigned long long t_chunk0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t i0 = c * 256 + lane;
     int a_ok[4], cidx[4];
     uint32_t rec[4];  // the four records of the lane
@@ -1397,6 +1481,10 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
         a_ok[q] = (int)(info & 1u);
         cidx[q] = (int)(info >> 1);
       }
+#ifdef AT2V_COMB_PROBE
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the first use waits for them in the product build)
+      probe.v[kCpBook] += __builtin_amdgcn_s_memtime() - t_chunk0;
+#endif
       all_hit = 1;
     } else {
       int hit = 1;
@@ -1421,18 +1509,21 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
       {
         gu_p3 P0, P1;
         ok[0] = comb2_point(P0, rec[0], n, pk, sig, msg, msg_total, off, policy, a_ok[0],
-                            comb + (size_t)cidx[0] * (kCombBytes / 16), tbc, sa, sr, lane);
+                            comb + (size_t)cidx[0] * (kCombBytes / 16), tbc, sa, sr, lane AT2V_CP_ARG);
         ok[1] = comb2_point(P1, rec[1], n, pk, sig, msg, msg_total, off, policy, a_ok[1],
-                            comb + (size_t)cidx[1] * (kCombBytes / 16), tbc, sa, sr, lane);
+                            comb + (size_t)cidx[1] * (kCombBytes / 16), tbc, sa, sr, lane AT2V_CP_ARG);
         fu_mulc(zz01, P0.Z, P1.Z);
         slot_store(slot, reinterpret_cast<const int32_t*>(&P0), 30);        // X, Y, Z (T not needed)
         slot_store(slot + 8, reinterpret_cast<const int32_t*>(&P1), 30);
       }
       gu_p3 P2, P3;
       ok[2] = comb2_point(P2, rec[2], n, pk, sig, msg, msg_total, off, policy, a_ok[2],
-                          comb + (size_t)cidx[2] * (kCombBytes / 16), tbc, sa, sr, lane);
+                          comb + (size_t)cidx[2] * (kCombBytes / 16), tbc, sa, sr, lane AT2V_CP_ARG);
       ok[3] = comb2_point(P3, rec[3], n, pk, sig, msg, msg_total, off, policy, a_ok[3],
-                          comb + (size_t)cidx[3] * (kCombBytes / 16), tbc, sa, sr, lane);
+                          comb + (size_t)cidx[3] * (kCombBytes / 16), tbc, sa, sr, lane AT2V_CP_ARG);
+#ifdef AT2V_COMB_PROBE
+      const unsigned long long t_fin0 = __builtin_amdgcn_s_memtime();
+#endif
       fu zz23, zz, inv, inv01, zi;
       fu_mulc(zz23, P2.Z, P3.Z);
       fu_mulc(zz, zz01, zz23);
@@ -1455,6 +1546,9 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
       load8(Rw, sig + (size_t)rec[1] * 64);
       fu_mulc(zi, inv01, Q0.Z);
       good[1] = ok[1] & gu_encode_eq_zi(Q1, zi, Rw);
+#ifdef AT2V_COMB_PROBE
+      probe.v[kCpFinish] += __builtin_amdgcn_s_memtime() - t_fin0;
+#endif
     } else {
       // one quarter at a time through ONE inlined copy of the ladder
 #pragma unroll 1
@@ -1474,6 +1568,9 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
         good[3] = q == 3 ? gq : good[3];
       }
     }
+#ifdef AT2V_COMB_PROBE
+    const unsigned long long t_book0 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if constexpr (kPart) {  // records in list order
@@ -1491,7 +1588,26 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
     if (lane == 0) ticket = atomicAdd(chunk_queue, 1u);
     ticket = __builtin_amdgcn_readfirstlane(ticket);
     c = ticket < nchunks ? nwaves + ticket : nchunks;
+#ifdef AT2V_COMB_PROBE
+    if constexpr (kPart) {
+      const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+      probe.v[kCpBook] += t_end - t_book0;
+      probe.v[kCpChunk] += t_end - t_chunk0;
+      probe.v[kCpChunks] += 1;
+      probe.v[kCpBWait] += tbc.waited;
+      probe.v[kCpStage] += tbc.stage_waited;
+      tbc.waited = tbc.stage_waited = 0;
+    }
+#endif
   }
+#ifdef AT2V_COMB_PROBE
+  if constexpr (kPart) {  // one vector atomic per counter and wave, from lane 0
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < kCpN; ++k) atomicAdd(&at2v_cprobe_acc[k], probe.v[k]);
+  }
+#endif
+#undef AT2V_CP_ARG
 }
 
 // the same with per-key combs (at2v_opts.sender_comb): all-hit waves verify by additions only
@@ -2350,3 +2466,17 @@ size_t scratch_bytes(int grid) { return (size_t)grid * scratch_bytes_per_block()
 int block_threads() { return kBlock; }
 
 }  // namespace at2v
+
+#ifdef AT2V_COMB_PROBE
+// probe builds only: copy out the comb kernel's probe sums (at2v::kCpN counters) and zero them
+extern "C" int at2v_probe_read(unsigned long long* out, int n) {
+  if (n < (int)at2v::kCpN) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(at2v::at2v_cprobe_acc), sizeof(unsigned long long) * at2v::kCpN) !=
+      hipSuccess)
+    return -3;
+  unsigned long long z[at2v::kCpN] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(at2v::at2v_cprobe_acc), z, sizeof(z)) != hipSuccess) return -4;
+  return (int)at2v::kCpN;
+}
+#endif

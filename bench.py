@@ -26,6 +26,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
 
 CFG_SEED = 0x4154325F
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """one line per phase on stderr (stdout carries only the JSON line): a long default run shows where it is"""
+    sys.stderr.write(f"[bench {time.perf_counter() - _T_START:7.1f} s] {msg}\n")
+    sys.stderr.flush()
+
 # Algorithmic work per verify (DESIGN.md §4b, half-size equation, 33-window chain): decode A and R
 # 510 S + 44 M, tables [j]A and [j](+-R) 128 M, ladder 32 x (16 S + 28 M) + top window 15 M + 8 fixed-base
 # windows x 14 M = 512 S + 1023 M; 1195 M + 1022 S in all. A 10-limb radix-2^25.5 multiplication is 100 and a
@@ -174,6 +182,7 @@ def main():
 
     import at2v
 
+    progress("torch and at2v imported")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -276,6 +285,7 @@ def main():
     barrier()
     launch_ms_alone = ea.elapsed_time(eb)
     kernel_ms_local, elapsed_local, launch_alone_local = kernel_ms, elapsed, launch_ms_alone
+    progress(f"timed steps done: {kernel_ms:.3f} ms per step on the device")
     elapsed, kernel_ms, launch_ms_alone = reduce([elapsed, kernel_ms, launch_ms_alone],
                                                  dist.ReduceOp.MAX if use_dist else None)
 
@@ -366,13 +376,18 @@ def main():
             out.update(e2e)
         if multi:
             out["multi_gpu"] = multi
+    if e2e:
+        progress("host-buffer leg done")
     if rank == 0 and world == 1 and args.traffic_leg and not args.senders and not use_dist:
+        progress("AT2-traffic leg")
         out["at2_traffic"] = at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L)
     if rank == 0 and world == 1 and args.churn_legs not in ("", "0") and not args.senders and not use_dist:
         out["sender_churn"] = churn_legs(args, at2v, torch, dev, lstreams, n, L, kernel_ms, value)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
+        progress("CPU baseline")
         out["cpu_baseline"] = cpu_baseline(args, d_pk, d_sig, d_msg, n, L)
     if rank == 0 and world == 1 and args.pmc_traffic and not use_dist:
+        progress("PMC passes")
         tr = pmc_traffic(args, n, L)
         if tr is not None:
             out["roofline"]["traffic"] = tr["bytes_per_launch"]
@@ -386,6 +401,7 @@ def main():
             out["roofline"]["valu_measured"] = vl
             out["effective_clock_ghz"] = vl["effective_clock_ghz"]
     if rank == 0:
+        progress("done")
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     v.close()
@@ -474,6 +490,7 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
     for name, keys_of in legs.items():
         if name not in args.churn_legs.split(","):
             continue
+        progress(f"churn leg {name}")
         v = at2v.BatchVerifier(device=dev.index or 0, policy=args.policy, sender_cache=1024, sender_comb=True)
         batches, key_bufs = [], []
         for b in range(nb):
@@ -498,10 +515,12 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
             v.verify_batch_device(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), n * L, b[3].data_ptr(), n,
                                   vers[j].data_ptr(), lstreams[j].cuda_stream)
 
+        progress(f"churn leg {name}: {nb} batches generated")
         for k in range(warm):
             step(k)
         torch.cuda.synchronize(dev)
         h0 = v.info()
+        progress(f"churn leg {name}: warm-up done")
         ev0 = torch.cuda.Event(enable_timing=True)
         kend = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
         t0 = time.perf_counter()
@@ -708,7 +727,8 @@ def _pmc_pass(args, n, L, counters):
            "--warmup", "2" if args.senders else "0",  # repeating senders: the keys are cached by the profiled steps
            "--cpu-sample", "0", "--pmc-traffic", "0", "--records-per-gpu", str(n), "--msg-len", str(L),
            "--policy", args.policy, "--senders", str(args.senders), "--sender-cache", str(args.sender_cache),
-           "--sender-comb", str(args.sender_comb), "--e2e", "0", "--traffic-leg", "0"]
+           "--sender-comb", str(args.sender_comb), "--e2e", "0", "--traffic-leg", "0", "--churn-legs", "0"]
+    progress(f"PMC pass {' '.join(counters)}")
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=150, check=True)
         rows, durs = [], []

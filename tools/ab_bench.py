@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="perf-only experiment builds: skip the verdict check")
     ap.add_argument("--senders", type=int, default=0, help="records signed by this many repeating senders (0 = distinct)")
     ap.add_argument("--comb", action="store_true", help="contexts with sender_cache 1024 + sender_comb (AT2 traffic)")
+    ap.add_argument("--probe", action="store_true",
+                    help="builds with -DAT2V_COMB_PROBE: print the comb kernel's per-wait cycle sums (rounds 2..)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L = a.n, a.msg_len
@@ -70,9 +72,37 @@ def main():
             if r > 0:
                 times[p].append(e0.elapsed_time(e1))
             assert ok or a.no_check, f"{p}: wrong verdicts"
+        if a.probe and r == 1:  # the warm-up launches (sighting, claims) are not counted
+            for lib, _ in libs:
+                if hasattr(lib, "at2v_probe_read"):
+                    probe_read(lib)
     for p in a.libs:
         t = np.array(times[p])
         print(f"{os.path.basename(p):28s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  -> {n / np.median(t) / 1e3:8.2f} M verifies/s")
+    if a.probe:
+        for p, (lib, _) in zip(a.libs, libs):
+            if hasattr(lib, "at2v_probe_read"):
+                print_probe(os.path.basename(p), probe_read(lib))
+
+
+PROBE_NAMES = ["A-comb entry waits (vmcnt)", "B-comb entry waits (vmcnt)", "stage refill waits (lgkmcnt)",
+               "record loads + prechecks", "SHA-512 + recode (msg loads incl.)", "comb additions (waits incl.)",
+               "slot + inversion + encodes", "list loads + verdicts + ticket", "chunk total", "chunks"]
+
+
+def probe_read(lib):
+    buf = (ctypes.c_ulonglong * 16)()
+    k = lib.at2v_probe_read(buf, 16)
+    assert k > 0, k
+    return [int(buf[i]) for i in range(k)]
+
+
+def print_probe(name, v):
+    """the comb kernel's wave-cycle sums (s_memtime) per phase and wait, as a share of the chunk total"""
+    tot, chunks = v[8], max(1, v[9])
+    print(f"probe {name}: {chunks} chunks of 256 records, {tot / chunks:.0f} wave-cycles per chunk")
+    for i in range(8):
+        print(f"  {PROBE_NAMES[i]:36s} {100.0 * v[i] / max(1, tot):6.2f} %  ({v[i] / chunks:10.0f} cycles per chunk)")
 
 
 if __name__ == "__main__":

@@ -27,6 +27,8 @@
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
 #   ab=<a,b,...>  tools/ab_bench.py over at2-node_amd/at2v/variants/libat2v_<a>.so ... (distinct keys)
 #   abcomb=<...>  the same on 64-sender traffic with combs
+#   cprobe=<...>  the same with --probe: per-wait cycle table of builds made with -DAT2V_COMB_PROBE (cprobex=: without
+#                 the verdict check, for timing-only experiment builds)
 set -o pipefail
 TAG=$1; shift
 D=gpurun_out/$TAG
@@ -71,7 +73,7 @@ for st in "$@"; do
                grep '^{' $D/torchrun3.txt > $D/torchrun3.json ;;
     rocprof) export AT2V_SCRATCH_SETS=1
              run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- \
-               python3 bench.py --steps 20 --warmup 3 --pmc-traffic 0 --cpu-sample 0 --e2e 0
+               python3 bench.py --steps 20 --warmup 3 --pmc-traffic 0 --cpu-sample 0 --e2e 0 --churn-legs 0
              unset AT2V_SCRATCH_SETS
              find $D/prof -name '*kernel_stats.csv' -exec cp {} $D/kernel_stats.csv \; ;;
     latab) for r in 1 2; do for v in 0 1; do
@@ -112,6 +114,9 @@ for st in "$@"; do
     abx=*) libs=""  # experiment builds (wrong verdicts allowed), distinct keys
           for v in $(echo "${st#abx=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
           run abx 900 python3 tools/ab_bench.py $libs --rounds 12 --no-check ;;
+    cprobe=*|cprobex=*) libs=""; chk=""; [ "${st%%=*}" = cprobex ] && chk="--no-check"
+          for v in $(echo "${st#*=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
+          run ${st%%=*} 900 python3 tools/ab_bench.py $libs --rounds 8 --senders 64 --comb --probe $chk ;;
     abcombx=*) libs=""  # experiment builds (wrong verdicts allowed)
           for v in $(echo "${st#abcombx=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
           run abcombx 900 python3 tools/ab_bench.py $libs --rounds 12 --senders 64 --comb --no-check ;;

@@ -6,7 +6,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 --pmc-traffic 0"
+B="python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 --pmc-traffic 0 --churn-legs 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 || exit 11
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace --output-format csv -d $OUT/pmc1 -o run -- $B > $OUT/pmc1.log 2>&1 || exit 12
