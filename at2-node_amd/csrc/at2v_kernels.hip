@@ -1427,6 +1427,9 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
 // kPart: the chunks are 256 entries of the classify kernel's hit list (every record cached), verdict bits set by atomic
 // OR; no ladder branch.
 template <bool kPart = false>
+#ifndef AT2V_COMB4_LOOP
+#define AT2V_COMB4_LOOP 1  // the four records of a lane through one copy of the per-record code (0: four unrolled copies)
+#endif
 __device__ AT2V_INLINE void verify_chunks_comb4(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
@@ -1503,6 +1506,61 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
     }
     const uint32_t lim = kPart ? nh : n;  // list / batch positions below lim are real
     int good[4] = {0, 0, 0, 0};
+#if AT2V_COMB4_LOOP
+    if (kPart || all_hit) {
+      // ONE inlined copy of the per-record work, run four times: R'_q = comb sums of record q, parked in the slot (X, Y,
+      // Z at granules 8q..8q+7). Four unrolled copies made the kernel 400 KB of code, whose hot loops (four copies of
+      // SHA-512 and of the A and B comb loops) did not share the instruction cache between waves at different records.
+      int okm = 0;
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t rq = q == 0 ? rec[0] : q == 1 ? rec[1] : q == 2 ? rec[2] : rec[3];
+        const int aq = q == 0 ? a_ok[0] : q == 1 ? a_ok[1] : q == 2 ? a_ok[2] : a_ok[3];
+        const int cq = q == 0 ? cidx[0] : q == 1 ? cidx[1] : q == 2 ? cidx[2] : cidx[3];
+        gu_p3 P;
+        const int okq = comb2_point(P, rq, n, pk, sig, msg, msg_total, off, policy, aq,
+                                    comb + (size_t)cq * (kCombBytes / 16), tbc, sa, sr, lane AT2V_CP_ARG);
+        okm |= okq << q;
+        slot_store(slot + 8 * q, reinterpret_cast<const int32_t*>(&P), 30);  // X, Y, Z (T not needed)
+      }
+#ifdef AT2V_COMB_PROBE
+      const unsigned long long t_fin0 = __builtin_amdgcn_s_memtime();
+#endif
+      // Montgomery's trick: 1/Z_q = Z_{q^1} / (Z_q Z_{q^1}), and 1/(Z0 Z1), 1/(Z2 Z3) from one inversion
+      fu inv01, inv23;
+      {
+        fu z0, z1, z2, z3, zz01, zz23, zz, inv;
+        slot_load(reinterpret_cast<int32_t*>(z0.v), slot + 5, 10);
+        slot_load(reinterpret_cast<int32_t*>(z1.v), slot + 8 + 5, 10);
+        slot_load(reinterpret_cast<int32_t*>(z2.v), slot + 16 + 5, 10);
+        slot_load(reinterpret_cast<int32_t*>(z3.v), slot + 24 + 5, 10);
+        fu_mulc(zz01, z0, z1);
+        fu_mulc(zz23, z2, z3);
+        fu_mulc(zz, zz01, zz23);
+        fu_invert(inv, zz);
+        fu_mulc(inv01, inv, zz23);
+        fu_mulc(inv23, inv, zz01);
+      }
+      int goodm = 0;
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t rq = q == 0 ? rec[0] : q == 1 ? rec[1] : q == 2 ? rec[2] : rec[3];
+        fu zp, zi;
+        gu_p2 Q;
+        slot_load(reinterpret_cast<int32_t*>(zp.v), slot + 8 * (q ^ 1) + 5, 10);  // the partner's Z
+        slot_load(reinterpret_cast<int32_t*>(&Q), slot + 8 * q, 30);
+        uint32_t Rw[8];
+        load8(Rw, sig + (size_t)rq * 64);
+        fu_mulc(zi, q < 2 ? inv01 : inv23, zp);
+        goodm |= (((okm >> q) & 1) & gu_encode_eq_zi(Q, zi, Rw)) << q;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) good[q] = (goodm >> q) & 1;
+#ifdef AT2V_COMB_PROBE
+      probe.v[kCpFinish] += __builtin_amdgcn_s_memtime() - t_fin0;
+#endif
+    } else
+#else
     if (kPart || all_hit) {
       int ok[4];
       fu zz01;
@@ -1549,7 +1607,9 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
 #ifdef AT2V_COMB_PROBE
       probe.v[kCpFinish] += __builtin_amdgcn_s_memtime() - t_fin0;
 #endif
-    } else {
+    } else
+#endif  // AT2V_COMB4_LOOP
+    {
       // one quarter at a time through ONE inlined copy of the ladder
 #pragma unroll 1
       for (int q = 0; q < 4; ++q) {
@@ -1632,7 +1692,150 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 #endif
 }
 
-// partitioned cached launches: the classify kernel's hit list by comb additions, four records per lane
+// The classify kernel's hit list by comb additions, kRecs records per lane (chunks of 64 kRecs list positions): each
+// record's R' = [k](-A) + [s]B is parked in the lane's slot (X, Y, Z at granules 8q..8q+7), then ONE inversion serves
+// all kRecs Z's (Montgomery's trick as a product tree: pair products zp, for 8 records quad products, the inverse of the
+// product, back down to 1 / (Z_2k Z_2k+1) at granules 8 kRecs + 3k), and each record is encoded with
+// 1 / Z_q = Z_{q^1} / (Z_q Z_{q^1}). Per record: 254/kRecs squarings of the inversion, (3 kRecs - 3)/kRecs + 2
+// products. Verdict bits go to the record's place in the bitmap (verdict_or).
+template <int kRecs>
+__device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const uint8_t* __restrict__ pk,
+                                             const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+                                             uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n,
+                                             int policy, uint32_t* __restrict__ verdicts, int4* __restrict__ scratch,
+                                             uint32_t* __restrict__ chunk_queue, const CacheArgs& cc,
+                                             const PartArgs& pp, uint32_t nh) {
+  static_assert(kRecs == 4 || kRecs == 8, "records per lane");
+  static_assert(8 * kRecs + 3 * (kRecs / 2) <= kLaneGranules, "the slot holds the parked points and pair inverses");
+  const int lane = threadIdx.x & 63;
+  const int wib = AT2V_UNIFORM(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  constexpr uint32_t kChunk = 64 * kRecs;
+  const uint32_t nchunks = (nh + kChunk - 1) / kChunk;
+  const int4* __restrict__ comb = cc.payload;
+  int4* slot = scratch + ((size_t)wave * 64 + lane) * kLaneGranules;
+  int4* const pinv = slot + 8 * kRecs;  // 1 / (Z_2k Z_2k+1), 3 granules each
+  int4* const sa = astage + wib * 640;
+  int4* const sr = rstage + wib * 640;
+  const DevBComb tbc{cc.bcomb, {sa, sr}, lane};
+  constexpr uint32_t kHalf = kWavesPerBlock / 2;
+  const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
+                                            : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
+  auto zload = [&](fu& z, int q) { slot_load(reinterpret_cast<int32_t*>(z.v), slot + 8 * q + 5, 10); };
+#ifdef AT2V_COMB_PROBE
+  CombProbe probe;
+  CombProbe* const pr = &probe;
+#endif
+  for (uint32_t c = c_first; c < nchunks;) {
+#ifdef AT2V_COMB_PROBE
+    const unsigned long long t_chunk0 = __builtin_amdgcn_s_memtime();
+#endif
+    const uint32_t i0 = c * kChunk + lane;
+    int okm = 0;
+#pragma unroll 1
+    for (int q = 0; q < kRecs; ++q) {
+      const uint32_t pos = i0 + 64 * q, pc = pos < nh ? pos : nh - 1;
+      const uint32_t rq = pp.hidx[pc], info = pp.hinfo[pc];
+      gu_p3 P;
+      const int okq = comb2_point(P, rq, n, pk, sig, msg, msg_total, off, policy, (int)(info & 1u),
+                                  comb + (size_t)(info >> 1) * (kCombBytes / 16), tbc, sa, sr, lane
+#ifdef AT2V_COMB_PROBE
+                                  , pr
+#endif
+      );
+      okm |= okq << q;
+      slot_store(slot + 8 * q, reinterpret_cast<const int32_t*>(&P), 30);  // X, Y, Z (T not needed)
+    }
+#ifdef AT2V_COMB_PROBE
+    const unsigned long long t_fin0 = __builtin_amdgcn_s_memtime();
+#endif
+    {
+      fu z0, z1, zp0, zp1, inv;
+      zload(z0, 0);
+      zload(z1, 1);
+      fu_mulc(zp0, z0, z1);
+      zload(z0, 2);
+      zload(z1, 3);
+      fu_mulc(zp1, z0, z1);
+      if constexpr (kRecs == 4) {
+        fu_mulc(z0, zp0, zp1);
+        fu_invert(inv, z0);
+        fu_mulc(z0, inv, zp1);  // 1 / (Z0 Z1)
+        slot_store(pinv, reinterpret_cast<const int32_t*>(z0.v), 10);
+        fu_mulc(z0, inv, zp0);  // 1 / (Z2 Z3)
+        slot_store(pinv + 3, reinterpret_cast<const int32_t*>(z0.v), 10);
+      } else {
+        fu zp2, zp3, zq0, zq1;
+        zload(z0, 4);
+        zload(z1, 5);
+        fu_mulc(zp2, z0, z1);
+        zload(z0, 6);
+        zload(z1, 7);
+        fu_mulc(zp3, z0, z1);
+        fu_mulc(zq0, zp0, zp1);
+        fu_mulc(zq1, zp2, zp3);
+        fu_mulc(z0, zq0, zq1);
+        fu_invert(inv, z0);
+        fu_mulc(z0, inv, zq1);  // 1 / (Z0 Z1 Z2 Z3)
+        fu_mulc(z1, z0, zp1);   // 1 / (Z0 Z1)
+        slot_store(pinv, reinterpret_cast<const int32_t*>(z1.v), 10);
+        fu_mulc(z1, z0, zp0);   // 1 / (Z2 Z3)
+        slot_store(pinv + 3, reinterpret_cast<const int32_t*>(z1.v), 10);
+        fu_mulc(z0, inv, zq0);  // 1 / (Z4 Z5 Z6 Z7)
+        fu_mulc(z1, z0, zp3);   // 1 / (Z4 Z5)
+        slot_store(pinv + 6, reinterpret_cast<const int32_t*>(z1.v), 10);
+        fu_mulc(z1, z0, zp2);   // 1 / (Z6 Z7)
+        slot_store(pinv + 9, reinterpret_cast<const int32_t*>(z1.v), 10);
+      }
+    }
+#pragma unroll 1
+    for (int q = 0; q < kRecs; ++q) {
+      const uint32_t pos = i0 + 64 * q, pc = pos < nh ? pos : nh - 1;
+      const uint32_t rq = pp.hidx[pc];
+      fu zp, ip, zi;
+      gu_p2 Q;
+      zload(zp, q ^ 1);  // the partner's Z
+      slot_load(reinterpret_cast<int32_t*>(ip.v), pinv + 3 * (q >> 1), 10);
+      slot_load(reinterpret_cast<int32_t*>(&Q), slot + 8 * q, 30);
+      uint32_t Rw[8];
+      load8(Rw, sig + (size_t)rq * 64);
+      fu_mulc(zi, ip, zp);
+      const int good = ((okm >> q) & 1) & gu_encode_eq_zi(Q, zi, Rw);
+      verdict_or(verdicts, rq, good, pos < nh, lane);
+    }
+#ifdef AT2V_COMB_PROBE
+    const unsigned long long t_book0 = __builtin_amdgcn_s_memtime();
+    probe.v[kCpFinish] += t_book0 - t_fin0;
+#endif
+    uint32_t ticket = 0;
+    if (lane == 0) ticket = atomicAdd(chunk_queue, 1u);
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    c = ticket < nchunks ? nwaves + ticket : nchunks;
+#ifdef AT2V_COMB_PROBE
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    probe.v[kCpBook] += t_end - t_book0;
+    probe.v[kCpChunk] += t_end - t_chunk0;
+    probe.v[kCpChunks] += 1;
+    probe.v[kCpBWait] += tbc.waited;
+    probe.v[kCpStage] += tbc.stage_waited;
+    tbc.waited = tbc.stage_waited = 0;
+#endif
+  }
+#ifdef AT2V_COMB_PROBE
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kCpN; ++k) atomicAdd(&at2v_cprobe_acc[k], probe.v[k]);
+#endif
+}
+
+// partitioned cached launches: the classify kernel's hit list by comb additions, four records per lane. AT2V_COMB_HITS8
+// = 1 runs eight per lane (one inversion for eight) once the list fills every wave with at least two four-record
+// chunks: 1.4% slower on 1M records from 64 senders (one 512-record chunk per wave leaves the chunk queue nothing to
+// balance).
+#ifndef AT2V_COMB_HITS8
+#define AT2V_COMB_HITS8 0  // 1 measured 1.4% slower on 1M records from 64 senders (profiles/r05n/abcomb.txt)
+#endif
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb_part(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
@@ -1640,8 +1843,14 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     PartArgs p) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
-  verify_chunks_comb4<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
-                            chunk_queue, c, &p);
+  (void)btab;
+  const uint32_t nh = __builtin_amdgcn_readfirstlane(p.counts[0]);
+  if (AT2V_COMB_HITS8 && nh > 256u * gridDim.x * kWavesPerBlock)
+    verify_comb_hits<8>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, chunk_queue, c,
+                        p, nh);
+  else
+    verify_comb_hits<4>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, chunk_queue, c,
+                        p, nh);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
