@@ -350,6 +350,8 @@ enum {
   kCpBook,      // list loads, verdict ORs, chunk ticket
   kCpChunk,     // chunk total
   kCpChunks,    // chunks (count)
+  kCpLds,       // comb entries: lgkmcnt wait after the stage's LDS reads (forced in the probe build)
+  kCpSlot,      // parked points: vmcnt wait after the slot loads of the inversion and encodes (forced likewise)
   kCpN
 };
 __device__ unsigned long long at2v_cprobe_acc[kCpN];
@@ -365,7 +367,7 @@ struct DevComb {
   int4* stage[2];    // this wave's two 10 KiB stages (wave-uniform)
   int lane;
 #ifdef AT2V_COMB_PROBE
-  mutable unsigned long long waited = 0, stage_waited = 0;
+  mutable unsigned long long waited = 0, stage_waited = 0, lds_waited = 0;
 #endif
   __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
     AT2V_CPROBE(stage_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));  // the stage's previous entry is read
@@ -391,6 +393,9 @@ struct DevComb {
       w[4 * q + 2] = v.z;
       w[4 * q + 3] = v.w;
     }
+#ifdef AT2V_COMB_PROBE
+    AT2V_CPROBE(lds_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));
+#endif
     int32_t* cw = reinterpret_cast<int32_t*>(&c);
 #pragma unroll
     for (int q = 0; q < (int)(sizeof(CombEntry) / 4); ++q) cw[q] = w[q];
@@ -401,7 +406,7 @@ struct DevBComb {
   int4* stage[2];
   int lane;
 #ifdef AT2V_COMB_PROBE
-  mutable unsigned long long waited = 0, stage_waited = 0;
+  mutable unsigned long long waited = 0, stage_waited = 0, lds_waited = 0;
 #endif
   __device__ AT2V_INLINE void prefetch(int st, int i, int j) const {
     AT2V_CPROBE(stage_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));
@@ -428,6 +433,9 @@ struct DevBComb {
       w[4 * q + 2] = v.z;
       w[4 * q + 3] = v.w;
     }
+#ifdef AT2V_COMB_PROBE
+    AT2V_CPROBE(lds_waited, asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));
+#endif
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
       n.ypx.v[k] = w[k];
@@ -967,15 +975,20 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 }
 
 // The classify kernel of a partitioned cached launch: one record per lane, a wave takes kClassifyGroups consecutive
-// 64-record groups. Every sender is looked up exactly as the round-4 kernels did in their chunk prologue
-// (cache_lookup_wave: claims, sightings, epochs); the wave then takes room in the two lists with one atomic per list and
-// writes its hits (index, payload, decode verdict) and misses in group order, and the block adds its statistics with
-// one atomic per counter. (One wave per group with per-wave atomics took 0.54-0.77 ms per 1M records: ~100k atomics on
-// a handful of control words, profiles/r05f.)
-constexpr int kClassifyGroups = 8;
+// 64-record groups (a block of 4 waves, 4 kClassifyGroups groups). Every sender is looked up exactly as the round-4
+// kernels did in their chunk prologue (cache_lookup_wave: claims, sightings, epochs); the block then takes room in the
+// two lists with one atomic per list and writes its hits (index, payload, decode verdict) and misses in group order,
+// and adds its statistics with one atomic per counter. (One wave per group with per-wave atomics took 0.54-0.77 ms per
+// 1M records: ~100k atomics on a handful of control words, profiles/r05f. Eight groups per wave and per-wave list
+// atomics: the same atomic count as now, but each wave ran eight dependent lookup chains one after the other.)
+#ifndef AT2V_CLASSIFY_GROUPS
+#define AT2V_CLASSIFY_GROUPS 2
+#endif
+constexpr int kClassifyGroups = AT2V_CLASSIFY_GROUPS;
 __global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c,
                                                              PartArgs p) {
   __shared__ uint32_t sstat[4][8];
+  __shared__ uint32_t sbase[2];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const uint32_t ngroups = (n + 63) / 64;
@@ -1005,14 +1018,36 @@ __global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __re
       chunk_hits += hm[g] == am[g] ? 1u : 0u;
     }
   }
-  const uint32_t nm = na - nh;
-  uint32_t hb = 0, mb = 0;
   if (lane == 0) {
-    if (nh) hb = atomicAdd(p.counts, nh);
-    if (nm) mb = atomicAdd(p.counts + 1, nm);
+    sstat[wib][0] = chunks;
+    sstat[wib][1] = chunk_hits;
+    sstat[wib][2] = nh;
+    sstat[wib][3] = st.found;
+    sstat[wib][4] = st.claimed;
+    sstat[wib][5] = st.failed;
+    sstat[wib][6] = st.sighted;
+    sstat[wib][7] = na - nh;
   }
-  hb = (uint32_t)__shfl((int)hb, 0);
-  mb = (uint32_t)__shfl((int)mb, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the block's room in the two lists
+    const uint32_t th = sstat[0][2] + sstat[1][2] + sstat[2][2] + sstat[3][2];
+    const uint32_t tm = sstat[0][7] + sstat[1][7] + sstat[2][7] + sstat[3][7];
+    sbase[0] = th ? atomicAdd(p.counts, th) : 0u;
+    sbase[1] = tm ? atomicAdd(p.counts + 1, tm) : 0u;
+  }
+  if (threadIdx.x < 7) {
+    const uint32_t v = sstat[0][threadIdx.x] + sstat[1][threadIdx.x] + sstat[2][threadIdx.x] + sstat[3][threadIdx.x];
+    const int k = threadIdx.x;
+    const int word = k == 0 ? kCtlChunks : k == 1 ? kCtlChunkHits : k == 2 ? kCtlRecHits : k == 3 ? kCtlFound
+                     : k == 4 ? kCtlClaimed : k == 5 ? kCtlFailed : kCtlSighted;
+    if (v) atomicAdd(c.ctl + word, (unsigned long long)v);
+  }
+  __syncthreads();
+  uint32_t hb = sbase[0], mb = sbase[1];
+  for (int w = 0; w < wib; ++w) {  // (wave-uniform) the earlier waves' shares of the block's room
+    hb += sstat[w][2];
+    mb += sstat[w][7];
+  }
   const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
   for (int g = 0; g < kClassifyGroups; ++g) {
@@ -1027,24 +1062,6 @@ __global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __re
     }
     hb += (uint32_t)__popcll(hm[g]);
     mb += (uint32_t)__popcll(mm);
-  }
-  if (lane == 0) {
-    sstat[wib][0] = chunks;
-    sstat[wib][1] = chunk_hits;
-    sstat[wib][2] = nh;
-    sstat[wib][3] = st.found;
-    sstat[wib][4] = st.claimed;
-    sstat[wib][5] = st.failed;
-    sstat[wib][6] = st.sighted;
-    sstat[wib][7] = 0;
-  }
-  __syncthreads();
-  if (threadIdx.x < 7) {
-    const uint32_t v = sstat[0][threadIdx.x] + sstat[1][threadIdx.x] + sstat[2][threadIdx.x] + sstat[3][threadIdx.x];
-    const int k = threadIdx.x;
-    const int word = k == 0 ? kCtlChunks : k == 1 ? kCtlChunkHits : k == 2 ? kCtlRecHits : k == 3 ? kCtlFound
-                     : k == 4 ? kCtlClaimed : k == 5 ? kCtlFailed : kCtlSighted;
-    if (v) atomicAdd(c.ctl + word, (unsigned long long)v);
   }
 }
 
@@ -1315,8 +1332,78 @@ __device__ AT2V_INLINE int comb2_point(gu_p3& P, uint32_t i, uint32_t n, const u
   if (pr) {
     pr->v[kCpAWait] += tc.waited;
     pr->v[kCpStage] += tc.stage_waited;
+    pr->v[kCpLds] += tc.lds_waited;
   }
 #endif
+  return ok;
+}
+
+// comb2_point with the record's offset and length already known (the hit loop loads them with the list) and the message
+// staged in LDS: its words go to the wave's second comb stage by LDS-DMA (one global_load_lds_dword per word, issued
+// together with the loads of R, S and A), so the record pays one memory latency before SHA-512 instead of one for its
+// loads and one per message block. Used when every lane's message (with one word of alignment slack) fits the stage's
+// kMsgStageWords words and ends 8 bytes before the buffer end (the unguarded reader's condition); returns -1 without
+// doing anything otherwise (the caller falls back to comb2_point).
+constexpr int kMsgStageWords = 40;  // the 10 KiB stage: 40 words x 64 lanes x 4 B
+__device__ AT2V_INLINE int comb2_point_staged(gu_p3& P, uint32_t ii, uint32_t o0, uint32_t len,
+                                              const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                              const uint8_t* __restrict__ msg, uint32_t msg_total, int policy, int a_ok,
+                                              const int4* __restrict__ comb_key, const DevBComb& tbc, int4* sa,
+                                              int4* sr, int lane
+#ifdef AT2V_COMB_PROBE
+                                              , CombProbe* pr = nullptr
+#endif
+) {
+  const uint32_t kl = (len >> 2) + 2;  // words 0 .. (len >> 2) + 1 of the aligned window (the reader reads j and j + 1)
+  const int fits = __builtin_amdgcn_readfirstlane(
+      __all((uint64_t)o0 + len + 8 <= (uint64_t)msg_total && kl <= (uint32_t)kMsgStageWords) ? 1 : 0);
+  if (!fits) return -1;
+  const int kw = wave_max_i32((int)kl);
+  const uint32_t* mw = reinterpret_cast<const uint32_t*>(msg + (o0 & ~3u));
+  uint32_t* const ml = reinterpret_cast<uint32_t*>(sr);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's earlier LDS reads are done
+#pragma unroll 1
+  for (int j = 0; j < kw; ++j)  // word j of every lane's window -> ml[j * 64 + lane] (a lane past its window re-reads
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mw + ((uint32_t)j < kl ? (uint32_t)j : kl - 1)),
+                                     (__attribute__((address_space(3))) void*)(ml + j * 64), 4, 0, 0);  // its last)
+  uint32_t Rw[8], Sw[8], Aw[8];
+  int ok;
+#ifdef AT2V_COMB_PROBE
+  unsigned long long dummy = 0;
+  unsigned long long& p_rec = pr ? pr->v[kCpRecord] : dummy;
+  (void)p_rec;
+#endif
+  AT2V_CPROBE(p_rec, {
+    load8(Rw, sig + (size_t)ii * 64);
+    load8(Sw, sig + (size_t)ii * 64 + 32);
+    load8(Aw, pk + (size_t)ii * 32);
+    ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged message words have landed
+  });
+  const uint32_t msh = (o0 & 3u) * 8;
+  auto staged = [=](uint32_t j) -> uint32_t {
+    return __builtin_amdgcn_alignbit(ml[(j + 1) * 64 + lane], ml[j * 64 + lane], msh);
+  };
+  const DevComb tc{comb_key, {sa, sr}, lane};
+#ifdef AT2V_COMB_PROBE
+  if (pr) {
+    uint32_t kd[kCombDigitWords], sd[8];
+    AT2V_CPROBE(pr->v[kCpSha], {
+      comb_k_digits(kd, Rw, Aw, len, staged);
+      sc_recode16(sd, Sw);
+    });
+    AT2V_CPROBE(pr->v[kCpSums], {
+      gu_p3_identity(P);
+      comb_sum<true>(P, kd, 0, kCombPos, tc);
+      comb_sum<false>(P, sd, 0, kBCombPos, tbc);
+    });
+    pr->v[kCpAWait] += tc.waited;
+    pr->v[kCpStage] += tc.stage_waited;
+    pr->v[kCpLds] += tc.lds_waited;
+    return ok;
+  }
+#endif
+  comb_point(P, Rw, Aw, Sw, len, staged, tc, tbc);
   return ok;
 }
 
@@ -1698,6 +1785,9 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 // product, back down to 1 / (Z_2k Z_2k+1) at granules 8 kRecs + 3k), and each record is encoded with
 // 1 / Z_q = Z_{q^1} / (Z_q Z_{q^1}). Per record: 254/kRecs squarings of the inversion, (3 kRecs - 3)/kRecs + 2
 // products. Verdict bits go to the record's place in the bitmap (verdict_or).
+#ifndef AT2V_COMB_MSG_STAGE
+#define AT2V_COMB_MSG_STAGE 1  // messages staged in LDS before SHA-512 (comb2_point_staged); 0: read word by word
+#endif
 template <int kRecs>
 __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const uint8_t* __restrict__ pk,
                                              const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -1732,18 +1822,55 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
     const unsigned long long t_chunk0 = __builtin_amdgcn_s_memtime();
 #endif
     const uint32_t i0 = c * kChunk + lane;
+#if AT2V_COMB_MSG_STAGE
+    // the chunk's list entries, then their records' offsets: two memory latencies per chunk, not per record
+    uint32_t lrec[kRecs], linfo[kRecs], lo0[kRecs], llen[kRecs];
+#pragma unroll
+    for (int q = 0; q < kRecs; ++q) {
+      const uint32_t pos = i0 + 64 * q, pc = pos < nh ? pos : nh - 1;
+      lrec[q] = pp.hidx[pc];
+      linfo[q] = pp.hinfo[pc];
+    }
+#pragma unroll
+    for (int q = 0; q < kRecs; ++q) {
+      lo0[q] = off[lrec[q]];
+      llen[q] = off[lrec[q] + 1] - lo0[q];
+    }
+#endif
     int okm = 0;
 #pragma unroll 1
     for (int q = 0; q < kRecs; ++q) {
+#if AT2V_COMB_MSG_STAGE
+      uint32_t rq = lrec[0], info = linfo[0], o0 = lo0[0], len = llen[0];
+#pragma unroll
+      for (int k = 1; k < kRecs; ++k)
+        if (q == k) {  // (selects: a runtime index into a register array would go to scratch)
+          rq = lrec[k];
+          info = linfo[k];
+          o0 = lo0[k];
+          len = llen[k];
+        }
+#else
       const uint32_t pos = i0 + 64 * q, pc = pos < nh ? pos : nh - 1;
       const uint32_t rq = pp.hidx[pc], info = pp.hinfo[pc];
+#endif
       gu_p3 P;
-      const int okq = comb2_point(P, rq, n, pk, sig, msg, msg_total, off, policy, (int)(info & 1u),
-                                  comb + (size_t)(info >> 1) * (kCombBytes / 16), tbc, sa, sr, lane
+      int okq = -1;
+#if AT2V_COMB_MSG_STAGE
+      okq = comb2_point_staged(P, rq, o0, len, pk, sig, msg, msg_total, policy, (int)(info & 1u),
+                               comb + (size_t)(info >> 1) * (kCombBytes / 16), tbc, sa, sr, lane
 #ifdef AT2V_COMB_PROBE
-                                  , pr
+                               , pr
 #endif
       );
+#endif
+      if (okq < 0)
+        okq = comb2_point(P, rq, n, pk, sig, msg, msg_total, off, policy, (int)(info & 1u),
+                          comb + (size_t)(info >> 1) * (kCombBytes / 16), tbc, sa, sr, lane
+#ifdef AT2V_COMB_PROBE
+                          , pr
+#endif
+        );
       okm |= okq << q;
       slot_store(slot + 8 * q, reinterpret_cast<const int32_t*>(&P), 30);  // X, Y, Z (T not needed)
     }
@@ -1754,9 +1881,15 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
       fu z0, z1, zp0, zp1, inv;
       zload(z0, 0);
       zload(z1, 1);
+#ifdef AT2V_COMB_PROBE
+      AT2V_CPROBE(probe.v[kCpSlot], asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
+#endif
       fu_mulc(zp0, z0, z1);
       zload(z0, 2);
       zload(z1, 3);
+#ifdef AT2V_COMB_PROBE
+      AT2V_CPROBE(probe.v[kCpSlot], asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
+#endif
       fu_mulc(zp1, z0, z1);
       if constexpr (kRecs == 4) {
         fu_mulc(z0, zp0, zp1);
@@ -1800,6 +1933,9 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
       slot_load(reinterpret_cast<int32_t*>(&Q), slot + 8 * q, 30);
       uint32_t Rw[8];
       load8(Rw, sig + (size_t)rq * 64);
+#ifdef AT2V_COMB_PROBE
+      AT2V_CPROBE(probe.v[kCpSlot], asm volatile("s_waitcnt vmcnt(0)" ::: "memory"));
+#endif
       fu_mulc(zi, ip, zp);
       const int good = ((okm >> q) & 1) & gu_encode_eq_zi(Q, zi, Rw);
       verdict_or(verdicts, rq, good, pos < nh, lane);
@@ -1819,7 +1955,8 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
     probe.v[kCpChunks] += 1;
     probe.v[kCpBWait] += tbc.waited;
     probe.v[kCpStage] += tbc.stage_waited;
-    tbc.waited = tbc.stage_waited = 0;
+    probe.v[kCpLds] += tbc.lds_waited;
+    tbc.waited = tbc.stage_waited = tbc.lds_waited = 0;
 #endif
   }
 #ifdef AT2V_COMB_PROBE

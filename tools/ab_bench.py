@@ -87,7 +87,8 @@ def main():
 
 PROBE_NAMES = ["A-comb entry waits (vmcnt)", "B-comb entry waits (vmcnt)", "stage refill waits (lgkmcnt)",
                "record loads + prechecks", "SHA-512 + recode (msg loads incl.)", "comb additions (waits incl.)",
-               "slot + inversion + encodes", "list loads + verdicts + ticket", "chunk total", "chunks"]
+               "slot + inversion + encodes", "list loads + verdicts + ticket", "chunk total", "chunks",
+               "comb-entry LDS reads (lgkmcnt, forced)", "slot + R loads in the finish (vmcnt, forced)"]
 
 
 def probe_read(lib):
@@ -101,7 +102,7 @@ def print_probe(name, v):
     """the comb kernel's wave-cycle sums (s_memtime) per phase and wait, as a share of the chunk total"""
     tot, chunks = v[8], max(1, v[9])
     print(f"probe {name}: {chunks} chunks of 256 records, {tot / chunks:.0f} wave-cycles per chunk")
-    for i in range(8):
+    for i in list(range(8)) + list(range(10, len(v))):
         print(f"  {PROBE_NAMES[i]:36s} {100.0 * v[i] / max(1, tot):6.2f} %  ({v[i] / chunks:10.0f} cycles per chunk)")
 
 
