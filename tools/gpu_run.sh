@@ -25,6 +25,7 @@
 #   fresh         tools/fresh_sweep.sh: config 5 with a stream of first-seen senders (queue p50/p99 per node)
 #   stall/stallat2 wave-cycle split (issue / issue-stall / s_waitcnt) of verify_kernel / verify_kernel_comb
 #   icache        tools/icache_pmc.sh: instruction-cache hits / misses of the comb and ladder kernels
+#   abchurn=<a,b> tools/ab_churn.sh: the bench's AT2-traffic and churn legs with variant a / b, alternating, 2 rounds
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
 #   ab=<a,b,...>  tools/ab_bench.py over at2-node_amd/at2v/variants/libat2v_<a>.so ... (distinct keys)
 #   abcomb=<...>  the same on 64-sender traffic with combs
@@ -104,6 +105,7 @@ for st in "$@"; do
     pmc) run pmc 1100 bash tools/profile.sh $TAG ;;
     stallat2) run stallat2 400 bash tools/stall_pmc_at2.sh $TAG ;;
     icache) run icache 400 bash tools/icache_pmc.sh $TAG ;;
+    abchurn=*) run abchurn 900 bash tools/ab_churn.sh $TAG $(echo "${st#abchurn=}" | tr ',' ' ') 2 ;;
     stall) run stall 300 bash tools/stall_pmc_quick.sh $TAG ;;
     latency) run latency 400 python3 tools/latency_probe.py --reps 100 --comb 1
              grep '^{' $D/latency.txt > $D/latency_comb1.json ;;
