@@ -497,3 +497,36 @@ def test_partition_switch_same_verdicts(at2v_mod, golden, monkeypatch, comb, par
         for rep in range(3):
             assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek), rep
             v.info()
+
+
+def test_comb_hits_staged_and_unstaged_messages(at2v_mod, oracle):
+    """The comb hit loop stages a record's message in LDS when every lane's message fits the stage (length up to ~150
+    bytes) and ends 8 bytes before the buffer end; any other wave reads word by word (comb2_point_staged returns -1).
+    64 cached senders, 4,096 records with message lengths 0..199 at every byte alignment (so some 64-record waves fit
+    and some do not), mutated records, and the last records' messages ending exactly at the buffer end: verdicts equal
+    the oracle's on the cold launch and on the warm (all-hit) ones."""
+    rng = np.random.default_rng(97)
+    S, n = 64, 4096
+    seeds = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(S)]
+    keys = [oracle.public_key(s) for s in seeds]
+    lens = rng.integers(0, 200, n)
+    lens[: n // 2] = rng.integers(0, 140, n // 2)  # the first half: waves that all fit (the staged path)
+    msgs = [bytes(rng.integers(0, 256, int(k), dtype=np.uint8)) for k in lens]
+    snd = rng.integers(0, S, n)
+    pk = np.array([np.frombuffer(keys[s], np.uint8) for s in snd])
+    sig = np.array([np.frombuffer(oracle.sign(seeds[s], m), np.uint8) for s, m in zip(snd, msgs)])
+    msg = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
+    bad = rng.choice(n, 300, replace=False)
+    sig[bad[:150], 5] ^= 0x10  # R changes
+    for i in bad[150:]:  # M changes (a byte inside, when there is one)
+        if lens[i]:
+            msg[off[i] + rng.integers(0, lens[i])] ^= 0x01
+    want = oracle.verify_batch(pk, sig, msg, off)
+    assert 0 < want.sum() < n
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=True, admit_first=True) as v:
+        for rep in range(3):
+            got = v.verify_batch(pk, sig, msg, off)
+            assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
+            info = v.info()
+        assert info["cache_record_hits"] >= 2 * n, info
