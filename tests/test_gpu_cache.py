@@ -411,7 +411,9 @@ def test_admission_repeating_senders_become_hits(at2v_mod, oracle, comb):
     assert rates[0][0] == 0 and rates[3][0] == rates[3][1] == 64, rates
 
 
-@pytest.mark.parametrize("small", [OFF, 0], ids=["throughput", "lat"])
+# (without combs, launches up to small_batch_max take the pair kernel, which does not use the cache: no tables-lat case)
+@pytest.mark.parametrize("comb,small", [(False, OFF), (True, OFF), (True, 0)],
+                         ids=["tables-throughput", "comb-throughput", "comb-lat"])
 def test_compaction_while_launches_overlap_on_two_streams(at2v_mod, oracle, comb, small):
     """device launches alternate over two streams (the two scratch sets let them overlap) while a
     16-key cache fills and compacts again and again. A compaction runs on the context's stream; launches issued meanwhile
@@ -419,8 +421,6 @@ def test_compaction_while_launches_overlap_on_two_streams(at2v_mod, oracle, comb
     the oracle's (a launch that probed a half-built table or popped a payload still held by a kept key would verify
     records against another key's comb or table)."""
     import torch
-    if small == 0 and not comb:
-        pytest.skip("without combs, launches up to small_batch_max take the pair kernel, which does not use the cache")
     pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()  # 64 senders > 16 keys of capacity
     rng = np.random.default_rng(47)
     batches = []
