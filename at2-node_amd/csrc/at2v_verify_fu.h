@@ -47,6 +47,13 @@ namespace at2v {
 #define AT2V_DECODE_LATE 0
 #endif
 
+// AT2V_DECODE_LOOP = 1 (round 5 experiment): the two decodes, and later the two table builds, as rolled loops over
+// {A, R} (one code copy each; the decoded points parked in their table slots across SHA-512 and the lattice reduction,
+// as AT2V_PARK_POINTS does). The comb kernel gained 6% from the same change to its per-record code.
+#ifndef AT2V_DECODE_LOOP
+#define AT2V_DECODE_LOOP 0
+#endif
+
 // AT2V_TAB_MADD = 1 (round 5): a table's base point is a decoded point, affine (Z = 1), so [j+1]P = [j]P + P is a mixed
 // addition with P's affine Niels form (y+x, y-x, 2dxy; the two sums carried, as the B tables' entries are): 3 products
 // instead of 4 per entry (D = Z1 * 2 Z2 becomes 2 Z1), 7 M fewer per table, 14 per verify. The operand classes are the
@@ -99,10 +106,27 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     ok &= enc_y_canonical(Aw) & !enc_small_order(Aw);
   }
   // V2: decode A and R; R must be canonical (y < p, not x = 0 with the sign bit)
-#if !AT2V_DECODE_LATE
+#if !AT2V_DECODE_LATE && !AT2V_DECODE_LOOP
   gu_p3 A, R;
 #endif
-#if AT2V_DECODE_LATE
+#if AT2V_DECODE_LOOP
+  {
+    int okd = 1;
+#pragma unroll 1
+    for (int q = (kCacheable && a_cached) ? 1 : 0; q < 2; ++q) {
+      uint32_t W[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) W[i] = q ? Rw[i] : Aw[i];
+      gu_p3 P;
+      okd &= gu_frombytes(P, W);
+      if (q) okd &= enc_y_canonical(Rw) & !(fu_iszero(P.X) & (int)(Rw[7] >> 31));
+      TabP& tp = q ? tr : ta;
+      tp.park(P);
+    }
+    ok &= okd;
+    if (kCacheable && a_cached) ok &= a_cached_ok;
+  }
+#elif AT2V_DECODE_LATE
   // (after the reduction, below)
 #elif AT2V_TABLES_EARLY
   // 1: both tables early; 2: A's table early, R kept live (its table after the reduction); 3: R's table early (sign of
@@ -133,7 +157,7 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   ok &= enc_y_canonical(Rw);
   ok &= !(fu_iszero(R.X) & (int)(Rw[7] >> 31));
 #endif
-#if AT2V_PARK_POINTS && !AT2V_TABLES_EARLY && !AT2V_DECODE_LATE
+#if AT2V_PARK_POINTS && !AT2V_TABLES_EARLY && !AT2V_DECODE_LATE && !AT2V_DECODE_LOOP
   // A and R are not used again until the tables are built (after SHA-512, the lattice reduction and the recoding), and
   // holding their 80 words through those phases is what makes the compiler spill (one scratch reload and wait per
   // word, ~50 of them at the table build). Park them in the lanes' table slots (entry 8, written last by the build)
@@ -181,7 +205,22 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
 
   // tables [j]A and [j](+-R), j = 0..8: one after the other (AT2V_TABLES_X2 = 0, the default since round 3: the pair's
   // extra live registers cost more in spills than its ILP gains, profiles/r03q), or as one interleaved pair
-#if AT2V_DECODE_LATE
+#if AT2V_DECODE_LOOP
+  const int rflip = 0;
+#pragma unroll 1
+  for (int q = (kCacheable && a_cached) ? 1 : 0; q < 2; ++q) {
+    TabP& tp = q ? tr : ta;
+    gu_p3 P;
+    tp.unpark(P);
+    if (q && hs.c1_neg) {
+      fu_neg(P.X, P.X, FU_KC);
+      fu_carry(P.X);
+      fu_neg(P.T, P.T, FU_KC);
+      fu_carry(P.T);
+    }
+    build_a_table_from(P, tp);
+  }
+#elif AT2V_DECODE_LATE
   const int rflip = 0;
   if (kCacheable && a_cached) {  // [j]A comes from the cache entry
     ok &= a_cached_ok;
