@@ -65,6 +65,7 @@ class _Opts(ctypes.Structure):
 
 CTX_CPU_FALLBACK = 1   # include/at2v.h AT2V_CTX_CPU_FALLBACK: a failed GPU batch (host buffers) re-runs on the CPU backend
 CTX_ADMIT_FIRST = 2    # include/at2v.h AT2V_CTX_ADMIT_FIRST: sender-cache keys claim a payload at their first sighting
+CTX_BCOMB_WIDE = 4     # include/at2v.h AT2V_CTX_BCOMB_WIDE: with combs, also a 24-bit-window comb of B (11.8 GB)
 
 
 SMALL_BATCH_DEFAULT = 32768     # include/at2v.h AT2V_SMALL_BATCH_DEFAULT
@@ -214,19 +215,21 @@ class BatchVerifier:
 
     def __init__(self, device: int = 0, num_gpus: int = 1, policy="dalek", small_batch_max: int = 0,
                  sender_cache: int = 0, sender_comb: bool = False, cpu_threads: int = 0, cpu_fallback: bool = False,
-                 admit_first: bool = False):
+                 admit_first: bool = False, bcomb_wide: bool = False):
         """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
         0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel.
         sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off).
         sender_comb: with sender_cache, also keep a comb of -A per cached key (1.7 MB of HBM each, plus one 67 MB comb
-        of B per context; include/at2v.h): chunks whose senders are all cached verify by table additions only
-        (at2v_comb.h), launches of every size.
+        of B per context; include/at2v.h): records whose sender is cached verify by table additions only (at2v_comb.h),
+        launches of every size. bcomb_wide: with sender_comb, also an 11.8 GB comb of B with 24-bit windows for the
+        throughput kernel (five additions fewer per cached record; AT2V_CTX_BCOMB_WIDE).
         num_gpus=0: the CPU batch backend (no device; cpu_threads host threads, 0 = every usable CPU).
         cpu_fallback: a GPU context re-runs a host-buffer batch on the CPU backend after a device error (same verdicts;
         info()["cpu_fallbacks"] counts it). admit_first: cache keys claim a payload at their first sighting."""
         self._lib = load_library()
         self.policy = _POLICIES[policy]
-        flags = (CTX_CPU_FALLBACK if cpu_fallback else 0) | (CTX_ADMIT_FIRST if admit_first else 0)
+        flags = ((CTX_CPU_FALLBACK if cpu_fallback else 0) | (CTX_ADMIT_FIRST if admit_first else 0)
+                 | (CTX_BCOMB_WIDE if bcomb_wide else 0))
         opts = _Opts(device, num_gpus, self.policy, small_batch_max, sender_cache, 1 if sender_comb else 0,
                      cpu_threads, flags)
         h = ctypes.c_void_p()

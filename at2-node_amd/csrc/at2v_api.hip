@@ -89,7 +89,7 @@ struct SenderCache {
   at2v::CacheArgs args{};
   DevBuf tags[2], entries[2];  // the live tag table / entries ([cur]) and the compaction target ([cur ^ 1])
   int cur = 0;
-  DevBuf payload, free_slots, used, ctl, bcomb, seen, claim_list[kClaimSlots];
+  DevBuf payload, free_slots, used, ctl, bcomb, bcomb_lat, seen, claim_list[kClaimSlots];
   // Builds run on the context's own stream (the shard's), which a caller's launches on its own streams never use: a
   // separate build stream would share one of the process's 4 hardware queues (GPU_MAX_HW_QUEUES, round robin) with a
   // caller's stream, whose next copy or launch then waited behind a 0.8 ms comb build (config 5 p99).
@@ -201,7 +201,7 @@ void free_cache(SenderCache*& c) {
   if (!c) return;
   if (c->build) (void)hipStreamSynchronize(c->build);  // (the shard's stream: destroyed with the shard)
   for (DevBuf* b : {&c->tags[0], &c->tags[1], &c->entries[0], &c->entries[1], &c->payload, &c->free_slots, &c->used,
-                    &c->ctl, &c->bcomb, &c->seen})
+                    &c->ctl, &c->bcomb, &c->bcomb_lat, &c->seen})
     b->release();
   for (DevBuf& b : c->claim_list) b.release();
   if (c->built) (void)hipEventDestroy(c->built);
@@ -219,7 +219,7 @@ void free_cache(SenderCache*& c) {
 // Per-sender cache for `capacity` distinct keys on the current device: 2x as many tag slots (open addressing at
 // load <= 1/2), one payload per key. AT2V_TEST_CACHE_FP_BITS (tests only) keeps that many fingerprint bits, so distinct
 // keys collide and the byte comparison in the verify kernels is exercised.
-int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit_first) {
+int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit_first, bool bcomb_wide) {
   SenderCache* c = new (std::nothrow) SenderCache;
   if (!c) return AT2V_E_OOM;
   s.cache = c;
@@ -263,10 +263,17 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit
   a.ctl = (unsigned long long*)c->ctl.p;
   a.seen = (unsigned long long*)c->seen.p;
   a.new_list = (uint4*)c->claim_list[0].p;
-  if (comb) {  // the comb of B, built once
-    AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes()));
-    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, s.stream));
-    a.bcomb = (const int4*)c->bcomb.p;
+  if (comb) {  // the comb of B (16-bit windows) and, with AT2V_CTX_BCOMB_WIDE, the wide one; built once
+    AT2V_TRY(c->bcomb_lat.ensure(at2v::bcomb_bytes(1)));
+    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb_lat.p, 1, s.stream));
+    a.bcomb = a.bcomb_lat = (const int4*)c->bcomb_lat.p;
+    a.bcomb_wide = 0;
+    if (bcomb_wide && at2v::bcomb_bits(0) != at2v::bcomb_bits(1)) {
+      AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes(0)));
+      AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, 0, s.stream));
+      a.bcomb = (const int4*)c->bcomb.p;
+      a.bcomb_wide = 1;
+    }
   }
   AT2V_TRY(at2v::launch_cache_init(a, s.stream));
   AT2V_TRY(hipStreamSynchronize(s.stream));
@@ -468,7 +475,7 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   if (opts) o = *opts;
   if (o.num_gpus < 0 || o.num_gpus > 64) return AT2V_E_INVALID;
   if (o.policy != AT2V_POLICY_DALEK_V1 && o.policy != AT2V_POLICY_LIBSODIUM_1_0_18) return AT2V_E_INVALID;
-  if (o.flags & ~(AT2V_CTX_CPU_FALLBACK | AT2V_CTX_ADMIT_FIRST)) return AT2V_E_INVALID;
+  if (o.flags & ~(AT2V_CTX_CPU_FALLBACK | AT2V_CTX_ADMIT_FIRST | AT2V_CTX_BCOMB_WIDE)) return AT2V_E_INVALID;
   if (o.num_gpus == 0) {  // the CPU batch backend: no HIP call at all
     at2v_ctx* c = new (std::nothrow) at2v_ctx;
     if (!c) return AT2V_E_OOM;
@@ -504,7 +511,7 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
     int rc = init_shard(c->shards[(size_t)g], alias ? (o.device + g) % ndev : o.device + g);
     if (rc == AT2V_OK && o.sender_cache)
       rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd(), o.sender_comb != 0,
-                      (o.flags & AT2V_CTX_ADMIT_FIRST) != 0);
+                      (o.flags & AT2V_CTX_ADMIT_FIRST) != 0, (o.flags & AT2V_CTX_BCOMB_WIDE) != 0);
     // the cross-rank failure flag of at2v_comm_init_rank / at2v_verify_batch_sharded (first device): allocated here,
     // so a rank whose communicator set-up fails can still join the outcome all-reduce
     if (rc == AT2V_OK && g == 0) rc = hip_code(c->status.ensure(4));

@@ -2,23 +2,23 @@
 //
 // AT2 senders issue consecutive sequences (/root/reference/src/bin/server/accounts/account.rs:36-43): one public key A
 // signs many payloads. For such a key the device keeps a comb of -A, C[i][j] = [j 2^(10i)](-A) for i = 0..25, j = 0..512
-// (affine Niels, or cached form with AT2V_COMB_NIELS=0), next to the context's comb of B, D[i][j] = [j 2^(16i)]B for
-// i = 0..15, j = 0..2^15 (affine Niels).
-// Then dalek's point R' = [k](-A) + [s]B is a sum of 26 + 16 table entries, no doublings:
+// (affine Niels, or cached form with AT2V_COMB_NIELS=0), next to the context's comb of B, D[i][j] = [j 2^(Wi)]B for
+// i = 0..kBCombPos-1, j = 0..2^(W-1) (affine Niels; W = 24: 11 positions).
+// Then dalek's point R' = [k](-A) + [s]B is a sum of 26 + 11 table entries, no doublings:
 //   k = sum_i e_i 2^(10i), e_i in [-512, 511] (sc_recode_w) ->  [k](-A) = sum_i +-C[i][|e_i|]
-//   s = sum_i f_i 2^(16i), f_i in [-2^15, 2^15) (sc_recode16) ->  [s]B   = sum_i +-D[i][|f_i|]
+//   s = sum_i f_i 2^(Wi), f_i in [-2^(W-1), 2^(W-1)) (bcomb_recode) ->  [s]B = sum_i +-D[i][|f_i|]
 // and the verdict is dalek's own comparison, enc(R') == R_bytes (the full-length form, DESIGN.md §4: no lattice
 // reduction, no decode of R). Any correct evaluation of [k](-A) + [s]B is the same group element, so the verdicts are
 // those of the ladder kernels (and of the oracle), for every key the comb was built from, small-order and mixed-order
 // keys included; a key that fails dalek's decode has verdict 0 whatever the comb holds.
 //
-// Cost per verify: 42 mixed additions (7 M) + one inversion (254 S + 11 M; shared by four records in the throughput
+// Cost per verify: 37 mixed additions (7 M; 42 with W = 16) + one inversion (254 S + 11 M; shared by four records in the throughput
 // kernel) + SHA-512, against the half-size ladder's 2 exponentiations + 2 tables + 33 windows: ~5x fewer
 // multiplications. The comb of one key is 26 x 513 x 128 B = 1.7 MB (10-bit windows), built once (comb_build_lane).
 //   TabC  : prefetch(stage, i, j) / load_prefetched(stage, CombEntry&)   entry C[i][j] of this lane's key
 //   TabBC : prefetch(stage, i, j) / load_prefetched(stage, gu_niels&)    entry D[i][j]
 // Two stages alternate: the entry of the next addition is fetched while this one is computed. The low-latency kernel
-// splits one record's work over four waves (decode R | 16 B entries | SHA-512 + 13 A entries | SHA-512 + 13 A entries)
+// splits one record's work over four waves (decode R | 11 B entries | SHA-512 + 13 A entries | SHA-512 + 13 A entries)
 // and compares R' with the decoded R projectively (comb_check_split).
 #pragma once
 #include "at2v_gu.h"
@@ -45,8 +45,31 @@ static_assert((kCombPos << kCombWideLog2) <= 256, "one 256-thread block builds a
 static_assert((kCombPos << kCombNarrowLog2) <= 64, "one wave builds a key's comb");
 constexpr int kCombWideMaxKeys = 256;  // new keys per launch up to which the wide builder runs (1,024 waves)
 constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
-constexpr int kBCombPos = 16;         // B comb positions (radix 2^16)
-constexpr int kBCombEntries = 32769;  // j = 0..2^15
+// The comb of B (one per context): signed radix-2^W digits of s, W = AT2V_BCOMB_BITS. W = 24 (default since round 5):
+// 11 positions x (2^23 + 1) entries, 11.8 GB of the 288 GB HBM, five additions fewer per record than W = 16 (16 positions
+// x (2^15 + 1) entries, 67 MB); W = 20: 13 positions, 872 MB. 64-sender traffic: 514.0 / 535.4 / 551.8 M/s for W = 16 /
+// 20 / 24 (profiles/r05v/abcomb.txt).
+// The low-latency kernel (one wave per part of a record, every access on its critical path) keeps reading a W = 16 comb
+// of B that stays in the MALL: its 64 lanes' random entries in an 11.8 GB table cost a page walk each (config 5's queue
+// p50 went from 0.15 to 0.43 ms with W = 24 there, profiles/r05w). A context with combs holds both tables.
+#ifndef AT2V_BCOMB_BITS
+#define AT2V_BCOMB_BITS 24
+#endif
+template <int W>
+struct BCombGeom {
+  static_assert(W == 16 || W == 20 || W == 24, "B comb window");
+  static constexpr int kPos = (254 + W - 1) / W;                // positions
+  static constexpr int kEntries = (1 << (W - 1)) + 1;           // j = 0..2^(W-1)
+  static constexpr int kDigitWords = W == 16 ? 8 : kPos;        // 16: two halfword digits per word
+  static constexpr size_t kBytes = (size_t)kPos * kEntries * 128;
+};
+constexpr int kBCombBits = AT2V_BCOMB_BITS;  // the throughput kernels' comb of B
+constexpr int kBCombLatBits = 16;            // the low-latency kernel's
+constexpr int kBCombPos = BCombGeom<kBCombBits>::kPos;
+constexpr int kBCombEntries = BCombGeom<kBCombBits>::kEntries;
+constexpr int kBCombDigitWords = BCombGeom<kBCombBits>::kDigitWords;
+constexpr int kBCombLatPos = BCombGeom<kBCombLatBits>::kPos;
+constexpr int kBCombLatDigitWords = BCombGeom<kBCombLatBits>::kDigitWords;
 // A-comb entry form. 1 (default since round 4): affine Niels (y+x, y-x, 2dxy), 30 words in 8 granules = one 128-byte
 // line, mixed additions (7 M); the builder normalises its lane's entries with one inversion (Montgomery's trick).
 // 0: cached (Y+X, Y-X, 2Z, 2dT), 40 words in 10 granules (two or three lines), 8 M additions.
@@ -130,17 +153,26 @@ AT2V_HD AT2V_INLINE void comb_k_digits(uint32_t kd[kCombDigitWords], const uint3
 AT2V_HD AT2V_INLINE int comb_adigit(const uint32_t kd[kCombDigitWords], int i) {
   return (int)((seln<kCombDigitWords>(kd, i >> 1) >> (16 * (i & 1))) & 0xffff) - (1 << (kCombBits - 1));
 }
-AT2V_HD AT2V_INLINE int comb_bdigit(const uint32_t sd[8], int i) {
-  return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000;
+template <int W = kBCombBits>
+AT2V_HD AT2V_INLINE int comb_bdigit(const uint32_t* sd, int i) {
+  if constexpr (W == 16) return (int)((sel8(sd, i >> 1) >> (16 * (i & 1))) & 0xffff) - 0x8000;
+  else return (int)seln<BCombGeom<W>::kDigitWords>(sd, i) - (1 << (W - 1));
+}
+// s (or t) -> the digits of a W-bit comb of B
+template <int W = kBCombBits>
+AT2V_HD AT2V_INLINE void bcomb_recode(uint32_t out[BCombGeom<W>::kDigitWords], const uint32_t s[8]) {
+  if constexpr (W == 16) sc_recode16(out, s);
+  else sc_recode_w<W>(out, s);
 }
 
 // acc += sum over positions i in [i0, i1) of the signed entry C[i][e_i] (A comb, kAComb: CombEntry) or D[i][f_i] (B
-// comb, affine Niels). The entry of addition m + 1 is fetched (into the other stage) while m is computed.
+// comb of Tab::kBits-bit windows, affine Niels). The entry of addition m + 1 is fetched (into the other stage) while m
+// is computed.
 template <bool kAComb, class Tab>
-AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int i1, const Tab& tab) {
+AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t* dig, int i0, int i1, const Tab& tab) {
   auto digit = [&](int i) {
     if constexpr (kAComb) return comb_adigit(dig, i);
-    else return comb_bdigit(dig, i);
+    else return comb_bdigit<Tab::kBits>(dig, i);
   };
   gu_p1p1 t;
   int e = digit(i0);
@@ -175,12 +207,12 @@ AT2V_HD AT2V_INLINE void comb_sum(gu_p3& acc, const uint32_t dig[8], int i0, int
 template <class TabC, class TabBC, class MsgWord>
 AT2V_HD AT2V_INLINE void comb_point(gu_p3& acc, const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8],
                                     uint32_t len, MsgWord msgword, const TabC& tc, const TabBC& tb) {
-  uint32_t kd[kCombDigitWords], sd[8];
+  uint32_t kd[kCombDigitWords], sd[BCombGeom<TabBC::kBits>::kDigitWords];
   comb_k_digits(kd, Rw, Aw, len, msgword);
-  sc_recode16(sd, Sw);
+  bcomb_recode<TabBC::kBits>(sd, Sw);
   gu_p3_identity(acc);
   comb_sum<true>(acc, kd, 0, kCombPos, tc);
-  comb_sum<false>(acc, sd, 0, kBCombPos, tb);
+  comb_sum<false>(acc, sd, 0, BCombGeom<TabBC::kBits>::kPos, tb);
 }
 
 // dalek-1.x verify of one record from the comb of its key (one lane per record: the throughput path).
@@ -188,15 +220,15 @@ template <class TabC, class TabBC, class MsgWord>
 AT2V_HD AT2V_INLINE int verify_comb_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                        MsgWord msgword, int policy, int a_ok, const TabC& tc, const TabBC& tb) {
   const int ok = comb_prechecks(Rw, Aw, Sw, policy, a_ok);
-  uint32_t kd[kCombDigitWords], sd[8];
+  uint32_t kd[kCombDigitWords], sd[BCombGeom<TabBC::kBits>::kDigitWords];
   comb_k_digits(kd, Rw, Aw, len, msgword);
-  sc_recode16(sd, Sw);
+  bcomb_recode<TabBC::kBits>(sd, Sw);
   AT2V_PHASE(2);
-  // V4: R' = [k](-A) + [s]B as the sum of the 32 A entries and the 16 B entries
+  // V4: R' = [k](-A) + [s]B as the sum of the kCombPos A entries and the kBCombPos B entries
   gu_p3 acc;
   gu_p3_identity(acc);
   comb_sum<true>(acc, kd, 0, kCombPos, tc);
-  comb_sum<false>(acc, sd, 0, kBCombPos, tb);
+  comb_sum<false>(acc, sd, 0, BCombGeom<TabBC::kBits>::kPos, tb);
   AT2V_PHASE(4);
   // V5/V6: dalek compares the compressed R' with the 32 bytes of R
   gu_p2 Rp;

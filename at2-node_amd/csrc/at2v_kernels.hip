@@ -401,8 +401,10 @@ struct DevComb {
     for (int q = 0; q < (int)(sizeof(CombEntry) / 4); ++q) cw[q] = w[q];
   }
 };
-struct DevBComb {
-  const int4* base;  // the context's comb of B
+template <int W>
+struct DevBCombW {
+  static constexpr int kBits = W;
+  const int4* base;  // the context's comb of B (W-bit windows)
   int4* stage[2];
   int lane;
 #ifdef AT2V_COMB_PROBE
@@ -414,7 +416,7 @@ struct DevBComb {
     i = 0;
     j = 1;
 #endif
-    const int4* src = base + ((size_t)i * kBCombEntries + j) * 8;
+    const int4* src = base + ((size_t)i * BCombGeom<W>::kEntries + j) * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
@@ -444,6 +446,8 @@ struct DevBComb {
     }
   }
 };
+using DevBCombWide = DevBCombW<kBCombBits>;    // AT2V_CTX_BCOMB_WIDE contexts' comb of B (the hit-list kernel)
+using DevBCombLat = DevBCombW<kBCombLatBits>;  // every context with combs (all other comb paths)
 
 __device__ AT2V_INLINE void stage_btab(int4* lds) {
   const int4* src = reinterpret_cast<const int4*>(AT2V_BTAB);
@@ -878,7 +882,7 @@ __device__ AT2V_INLINE void verify_chunks(
       if (kComb) {
         if (all_hit) {
           const DevComb tc{cc.payload + (size_t)u * (kCombBytes / 16), {astage + wib * 640, rstage + wib * 640}, lane};
-          const DevBComb tbc{cc.bcomb, {astage + wib * 640, rstage + wib * 640}, lane};
+          const DevBCombLat tbc{cc.bcomb_lat, {astage + wib * 640, rstage + wib * 640}, lane};
           good = verify_comb_fu(Rw, Aw, Sw, len, msgword, policy, a_ok, tc, tbc) & act;
         } else {
           good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & act;
@@ -1077,9 +1081,9 @@ constexpr int kSplitPb = 80 * 64;     // -[t]B, cached form (40 words)
 // the same branch. A chunk whose records all hit splits each record's work by wave (at2v_comb.h, comb_check_split):
 //   wave 0: decode R and check its canonicity (one exponentiation), then, after the barrier, R' = Pa0 + Pa1 + Pb and
 //           the projective comparison -> verdict words
-//   wave 1: s < l, the 16 B-comb additions -> Pb
+//   wave 1: s < l, the kBCombPos (11) B-comb additions -> Pb
 //   wave 2: SHA-512 -> k, A-comb positions 0..15 -> Pa0;   wave 3: SHA-512 -> k, positions 16..31 -> Pa1
-// so a record's latency is the longest part (SHA-512 + 16 additions) instead of SHA-512 + 48 additions + an inversion.
+// so a record's latency is the longest part (SHA-512 + 13 additions) instead of SHA-512 + 37 additions + an inversion.
 // Any other chunk (a sender seen for the first time: its comb is built on the build stream after this launch and serves
 // later launches; a claim without a payload; a probe failure) runs the half-size check V = [c0]A + [c1]R - [t]B = 0
 //  split over the four waves: wave 0 decodes A and builds [j]A, wave 1 decodes R and builds [j]R while
@@ -1146,7 +1150,7 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
                                                                                         msg_guarded, touched};
     gu_p3 R;   // all-hit: wave 0's decoded R;  fallback: wave 0's decoded A, then [c0]A
     int ok0 = 0;
-    uint32_t td[8];  // fallback, wave 2: t's signed radix-2^16 digits
+    uint32_t td[kBCombLatDigitWords];  // fallback, wave 2: t's digits for the (low-latency) comb of B
     int4* slot = scratch + (((size_t)blockIdx.x * kWavesPerBlock + w) * 64 + lane) * kLaneGranules;
     const DevTabA tp{slot, st0, lane, btab + (size_t)kNumBtabs * kBtabEntries * 8};
     if (all_hit) {
@@ -1157,10 +1161,10 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
         gu_p3_identity(P);
         if (w == 1) {
           sok[lane] = (uint32_t)sc_is_canonical(Sw);
-          uint32_t sd[8];
-          sc_recode16(sd, Sw);
-          const DevBComb tb{c.bcomb, {st0, st1}, lane};
-          comb_sum<false>(P, sd, 0, kBCombPos, tb);
+          uint32_t sd[kBCombLatDigitWords];
+          bcomb_recode<kBCombLatBits>(sd, Sw);
+          const DevBCombLat tb{c.bcomb_lat, {st0, st1}, lane};
+          comb_sum<false>(P, sd, 0, kBCombLatPos, tb);
         } else {
           uint32_t kd[kCombDigitWords];
           comb_k_digits(kd, Rw, Aw, len, msgword);
@@ -1209,7 +1213,7 @@ __global__ __launch_bounds__(kLatBlock, 1) void verify_comb_lat_kernel(
         }
       } else if (w == 2) {
         gu_cached cm;
-        split_neg_tb(cm, td, DevBComb{c.bcomb, {st0, st1}, lane});  // -[t]B
+        split_neg_tb(cm, td, DevBCombLat{c.bcomb_lat, {st0, st1}, lane});  // -[t]B
         const uint32_t* cw = reinterpret_cast<const uint32_t*>(&cm);
 #pragma unroll
         for (int q = 0; q < 40; ++q) part[kSplitPb + q * 64 + lane] = cw[q];
@@ -1282,10 +1286,11 @@ __device__ AT2V_INLINE int with_msg_reader(const uint8_t* __restrict__ msg, uint
 }
 
 // R' of record i (clamped to the batch) from its key's comb; returns the checks that need no point arithmetic
+template <class TabBC>
 __device__ AT2V_INLINE int comb2_point(gu_p3& P, uint32_t i, uint32_t n, const uint8_t* __restrict__ pk,
                                        const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                        uint32_t msg_total, const uint32_t* __restrict__ off, int policy, int a_ok,
-                                       const int4* __restrict__ comb_key, const DevBComb& tbc, int4* sa, int4* sr,
+                                       const int4* __restrict__ comb_key, const TabBC& tbc, int4* sa, int4* sr,
                                        int lane
 #ifdef AT2V_COMB_PROBE
                                        , CombProbe* pr = nullptr
@@ -1312,15 +1317,15 @@ __device__ AT2V_INLINE int comb2_point(gu_p3& P, uint32_t i, uint32_t n, const u
   with_msg_reader(msg, msg_total, o0, len, [&](auto& mwd) {
 #ifdef AT2V_COMB_PROBE
     if (pr) {  // comb_point with its two phases timed apart
-      uint32_t kd[kCombDigitWords], sd[8];
+      uint32_t kd[kCombDigitWords], sd[BCombGeom<TabBC::kBits>::kDigitWords];
       AT2V_CPROBE(pr->v[kCpSha], {
         comb_k_digits(kd, Rw, Aw, len, mwd);
-        sc_recode16(sd, Sw);
+        bcomb_recode<TabBC::kBits>(sd, Sw);
       });
       AT2V_CPROBE(pr->v[kCpSums], {
         gu_p3_identity(P);
         comb_sum<true>(P, kd, 0, kCombPos, tc);
-        comb_sum<false>(P, sd, 0, kBCombPos, tbc);
+        comb_sum<false>(P, sd, 0, BCombGeom<TabBC::kBits>::kPos, tbc);
       });
       return 0;
     }
@@ -1345,10 +1350,11 @@ __device__ AT2V_INLINE int comb2_point(gu_p3& P, uint32_t i, uint32_t n, const u
 // kMsgStageWords words and ends 8 bytes before the buffer end (the unguarded reader's condition); returns -1 without
 // doing anything otherwise (the caller falls back to comb2_point).
 constexpr int kMsgStageWords = 40;  // the 10 KiB stage: 40 words x 64 lanes x 4 B
+template <class TabBC>
 __device__ AT2V_INLINE int comb2_point_staged(gu_p3& P, uint32_t ii, uint32_t o0, uint32_t len,
                                               const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
                                               const uint8_t* __restrict__ msg, uint32_t msg_total, int policy, int a_ok,
-                                              const int4* __restrict__ comb_key, const DevBComb& tbc, int4* sa,
+                                              const int4* __restrict__ comb_key, const TabBC& tbc, int4* sa,
                                               int4* sr, int lane
 #ifdef AT2V_COMB_PROBE
                                               , CombProbe* pr = nullptr
@@ -1387,15 +1393,15 @@ __device__ AT2V_INLINE int comb2_point_staged(gu_p3& P, uint32_t ii, uint32_t o0
   const DevComb tc{comb_key, {sa, sr}, lane};
 #ifdef AT2V_COMB_PROBE
   if (pr) {
-    uint32_t kd[kCombDigitWords], sd[8];
+    uint32_t kd[kCombDigitWords], sd[BCombGeom<TabBC::kBits>::kDigitWords];
     AT2V_CPROBE(pr->v[kCpSha], {
       comb_k_digits(kd, Rw, Aw, len, staged);
-      sc_recode16(sd, Sw);
+      bcomb_recode<TabBC::kBits>(sd, Sw);
     });
     AT2V_CPROBE(pr->v[kCpSums], {
       gu_p3_identity(P);
       comb_sum<true>(P, kd, 0, kCombPos, tc);
-      comb_sum<false>(P, sd, 0, kBCombPos, tbc);
+      comb_sum<false>(P, sd, 0, BCombGeom<TabBC::kBits>::kPos, tbc);
     });
     pr->v[kCpAWait] += tc.waited;
     pr->v[kCpStage] += tc.stage_waited;
@@ -1431,7 +1437,7 @@ __device__ AT2V_INLINE void verify_chunks_comb2(
   DevTabA tr{slot + kTabAGranules, sr, lane, ident};
   const DevTabB tb0{btab, sa, lane};
   const DevTabB tb1{btab + (size_t)kBtabEntries * 8, sr, lane};
-  const DevBComb tbc{cc.bcomb, {sa, sr}, lane};
+  const DevBCombLat tbc{cc.bcomb_lat, {sa, sr}, lane};
   auto wmax = [](int v) { return wave_max_i32(v); };
   constexpr uint32_t kHalf = kWavesPerBlock / 2;
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
@@ -1541,7 +1547,7 @@ __device__ AT2V_INLINE void verify_chunks_comb4(
   DevTabA tr{slot + kTabAGranules, sr, lane, ident};
   const DevTabB tb0{btab, sa, lane};
   const DevTabB tb1{btab + (size_t)kBtabEntries * 8, sr, lane};
-  const DevBComb tbc{cc.bcomb, {sa, sr}, lane};
+  const DevBCombLat tbc{cc.bcomb_lat, {sa, sr}, lane};
   auto wmax = [](int v) { return wave_max_i32(v); };
   constexpr uint32_t kHalf = kWavesPerBlock / 2;
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
@@ -1788,7 +1794,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 #ifndef AT2V_COMB_MSG_STAGE
 #define AT2V_COMB_MSG_STAGE 1  // messages staged in LDS before SHA-512 (comb2_point_staged); 0: read word by word
 #endif
-template <int kRecs>
+template <int kRecs, int kBW>
 __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const uint8_t* __restrict__ pk,
                                              const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                              uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n,
@@ -1808,7 +1814,8 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
   int4* const pinv = slot + 8 * kRecs;  // 1 / (Z_2k Z_2k+1), 3 granules each
   int4* const sa = astage + wib * 640;
   int4* const sr = rstage + wib * 640;
-  const DevBComb tbc{cc.bcomb, {sa, sr}, lane};
+  // the context's wide comb of B (AT2V_CTX_BCOMB_WIDE, 24-bit windows: five additions fewer) or the 16-bit one
+  const DevBCombW<kBW> tbc{kBW == kBCombLatBits ? cc.bcomb_lat : cc.bcomb, {sa, sr}, lane};
   constexpr uint32_t kHalf = kWavesPerBlock / 2;
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
                                             : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
@@ -1982,12 +1989,15 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   (void)btab;
   const uint32_t nh = __builtin_amdgcn_readfirstlane(p.counts[0]);
-  if (AT2V_COMB_HITS8 && nh > 256u * gridDim.x * kWavesPerBlock)
-    verify_comb_hits<8>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, chunk_queue, c,
-                        p, nh);
+  if (c.bcomb_wide)
+    verify_comb_hits<4, kBCombBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+                                    chunk_queue, c, p, nh);
+  else if (AT2V_COMB_HITS8 && nh > 256u * gridDim.x * kWavesPerBlock)
+    verify_comb_hits<8, kBCombLatBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+                                       chunk_queue, c, p, nh);
   else
-    verify_comb_hits<4>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, chunk_queue, c,
-                        p, nh);
+    verify_comb_hits<4, kBCombLatBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+                                       chunk_queue, c, p, nh);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -2580,19 +2590,21 @@ __global__ __launch_bounds__(256) void cache_freelist_kernel(CacheArgs c, CacheC
     if (!x.used[u]) c.free_slots[atomicAdd(c.ctl + kCtlFreeCount, 1ull)] = u;
 }
 
-// D[pos][j] = [j 2^(16 pos)]B, j = 0..2^15, affine Niels on the unsigned field: one lane per entry, (j 2^(16 pos)) mod l
-// through the signed-field base ladder (as build_btab_kernel), built once per context with combs on.
-__global__ __launch_bounds__(kBlock) void build_bcomb_kernel(int4* __restrict__ out, int pos) {
+// D[pos][j] = [j 2^(W pos)]B, j = 0..2^(W-1) (W = kBCombBits), affine Niels on the unsigned field: one lane per entry,
+// (j 2^(W pos)) mod l through the signed-field base ladder (as build_btab_kernel), built once per context with combs on.
+__global__ __launch_bounds__(kBlock) void build_bcomb_kernel(int4* __restrict__ out, int bits, int pos) {
   __shared__ int4 btab[AT2V_BTAB_ENTRIES * 8];
   stage_btab(btab);
   LdsTabB tb{btab};
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= (uint32_t)kBCombEntries) return;
+  const uint32_t entries = (1u << (bits - 1)) + 1;
+  if (j >= entries) return;
   uint32_t x[16], k[8];
 #pragma unroll
   for (int q = 0; q < 16; ++q) x[q] = 0;
-  const int bit = 16 * pos;
-  x[bit >> 5] = j << (bit & 31);  // j <= 2^15: the halfword at bit 16 pos fits its word
+  const int bit = bits * pos, wk = bit >> 5, sh = bit & 31;
+  x[wk] = j << sh;  // j <= 2^(W-1): W bits at bit W pos, across two words when they straddle one
+  if (sh + bits > 32) x[wk + 1] = j >> (32 - sh);
   sc_reduce512(k, x);
   ge_p2 P;
   ge_scalarmult_base(P, k, tb);
@@ -2608,18 +2620,21 @@ __global__ __launch_bounds__(kBlock) void build_bcomb_kernel(int4* __restrict__ 
     w[20 + q] = (int32_t)nu.xy2d.v[q];
   }
   w[30] = w[31] = 0;
-  int4* dst = out + ((size_t)pos * kBCombEntries + j) * 8;
+  int4* dst = out + ((size_t)pos * entries + j) * 8;
 #pragma unroll
   for (int q = 0; q < 8; ++q) dst[q] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
 size_t cache_entry_bytes() { return (size_t)kCacheEntryGranules * 16; }
 size_t cache_payload_bytes(int comb) { return comb ? kCombBytes : (size_t)kTabAGranules * 16; }
-size_t bcomb_bytes() { return (size_t)kBCombPos * kBCombEntries * 8 * 16; }
+size_t bcomb_bytes(int lat) { return lat ? BCombGeom<kBCombLatBits>::kBytes : BCombGeom<kBCombBits>::kBytes; }
+int bcomb_bits(int lat) { return lat ? kBCombLatBits : kBCombBits; }
 
-hipError_t launch_build_bcomb(int4* out, hipStream_t stream) {
-  for (int pos = 0; pos < kBCombPos; ++pos) {
-    hipLaunchKernelGGL(build_bcomb_kernel, dim3((kBCombEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out,
+hipError_t launch_build_bcomb(int4* out, int lat, hipStream_t stream) {
+  const int bits = bcomb_bits(lat), npos = (254 + bits - 1) / bits;
+  const uint32_t entries = (1u << (bits - 1)) + 1;
+  for (int pos = 0; pos < npos; ++pos) {
+    hipLaunchKernelGGL(build_bcomb_kernel, dim3((entries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out, bits,
                        pos);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

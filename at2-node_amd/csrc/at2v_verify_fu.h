@@ -598,7 +598,8 @@ AT2V_HD AT2V_INLINE int split_r_side(const uint32_t Rw[8], TabP& tp) {
 // digits of c0 and |c1| (sc_recode4_hi8), t = c1 s mod l (sc_recode16), the sign of c1 and the lane's window count;
 // returns 0 for a lane whose scalars would need a 65th window (fails closed, as verify_half_fu)
 template <class MsgWord>
-AT2V_HD AT2V_INLINE int split_scalars(uint32_t c0d[8], uint32_t c1d[8], uint32_t td[8], int& c1_neg, int& nw_lane,
+AT2V_HD AT2V_INLINE int split_scalars(uint32_t c0d[8], uint32_t c1d[8], uint32_t td[kBCombLatDigitWords], int& c1_neg,
+                                      int& nw_lane,
                                       const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                       MsgWord msgword) {
   uint32_t k[8];
@@ -621,7 +622,7 @@ AT2V_HD AT2V_INLINE int split_scalars(uint32_t c0d[8], uint32_t c1d[8], uint32_t
   sc_mul_signed(t, hs, Sw);
   sc_recode4_hi8(c0d, hs.c0);
   sc_recode4_hi8(c1d, hs.c1);
-  sc_recode16(td, t);
+  bcomb_recode<kBCombLatBits>(td, t);  // (the low-latency comb of B's digits: -[t]B comes from it, split_neg_tb)
   c1_neg = hs.c1_neg;
   const int ok = hs.bits <= 255;
   nw_lane = ok ? hs.bits / 4 + 1 : 0;
@@ -630,10 +631,10 @@ AT2V_HD AT2V_INLINE int split_scalars(uint32_t c0d[8], uint32_t c1d[8], uint32_t
 
 // -[t]B in cached form, from the comb of B (TabBC: prefetch(stage, i, j) / load_prefetched(stage, gu_niels&))
 template <class TabBC>
-AT2V_HD AT2V_INLINE void split_neg_tb(gu_cached& out, const uint32_t td[8], const TabBC& tb) {
+AT2V_HD AT2V_INLINE void split_neg_tb(gu_cached& out, const uint32_t* td, const TabBC& tb) {
   gu_p3 P;
   gu_p3_identity(P);
-  comb_sum<false>(P, td, 0, kBCombPos, tb);
+  comb_sum<false>(P, td, 0, BCombGeom<TabBC::kBits>::kPos, tb);
   gu_p3_to_cached(out, P);
   gu_cached_cneg(out, 1);
 }

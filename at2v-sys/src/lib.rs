@@ -84,7 +84,7 @@ pub struct At2vOpts {
     pub sender_comb: u32,
     /// host threads of the CPU backend (num_gpus = 0, or AT2V_CTX_CPU_FALLBACK); 0 = every usable CPU
     pub cpu_threads: u32,
-    /// AT2V_CTX_CPU_FALLBACK | AT2V_CTX_ADMIT_FIRST
+    /// AT2V_CTX_CPU_FALLBACK | AT2V_CTX_ADMIT_FIRST | AT2V_CTX_BCOMB_WIDE
     pub flags: u32,
 }
 
@@ -99,6 +99,8 @@ impl Default for At2vOpts {
 pub const AT2V_CTX_CPU_FALLBACK: u32 = 1;
 /// `At2vOpts::flags`: sender-cache keys claim a payload at their first sighting (default: the second).
 pub const AT2V_CTX_ADMIT_FIRST: u32 = 2;
+/// `At2vOpts::flags`: with sender_comb, also an 11.8 GB comb of B (24-bit windows) for the throughput kernel.
+pub const AT2V_CTX_BCOMB_WIDE: u32 = 4;
 
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
 pub const AT2V_SMALL_BATCH_OFF: u32 = 0xffffffff;

@@ -46,10 +46,11 @@ MAC_PER_VERIFY = 100 * FIELD_MUL_PER_VERIFY + 55 * FIELD_SQ_PER_VERIFY  # 175,71
 # VALU rate on gfx950 (profiles/r01_ubench_valu.txt): one wave64 instruction per 4 cycles per SIMD
 # = 16 lane-MACs/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz.
 MAC_PEAK = 256 * 4 * 16 * 2.4e9  # 3.93e13 MAC/s
-# The comb path of AT2 traffic (DESIGN.md §10d, 10-bit A windows, four records per lane): 26 + 16 mixed additions with
-# affine entries (7 M), a quarter of a shared inversion (254 S + 11 M) + 2.25 M of Montgomery's trick over four Z's,
-# and 2 M to encode R': 301 M + 63.5 S per verify.
-COMB_MAC_PER_VERIFY = 100 * 301 + 55 * 63.5  # 33,592.5
+# The comb path of AT2 traffic (DESIGN.md §10d, 10-bit A windows and the wide comb of B's 24-bit windows, four records
+# per lane, the bench's at2_traffic leg: a context with AT2V_CTX_BCOMB_WIDE): 26 + 11
+# mixed additions with affine entries (7 M), a quarter of a shared inversion (254 S + 11 M) + 2.25 M of Montgomery's
+# trick over four Z's, and 2 M to encode R': 266 M + 63.5 S per verify (round 4's 16-bit B windows: 301 M + 63.5 S).
+COMB_MAC_PER_VERIFY = 100 * 266 + 55 * 63.5  # 30,092.5
 HBM_PEAK_GBS = 8000.0
 
 
@@ -415,7 +416,10 @@ def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
     i % senders), verified through a context with the per-sender cache and combs; the combs are built by the first
     (warm-up) launch. Same step structure as the headline (overlapped launches on the two streams). Reported beside the
     headline value, which stays the distinct-key workload of BASELINE config 2."""
-    v = at2v.BatchVerifier(device=dev.index or 0, policy=args.policy, sender_cache=1024, sender_comb=True)
+    t_create = time.perf_counter()
+    v = at2v.BatchVerifier(device=dev.index or 0, policy=args.policy, sender_cache=1024, sender_comb=True,
+                           bcomb_wide=True)
+    t_create = time.perf_counter() - t_create
     bufs = [torch.empty(n * 32, dtype=torch.uint8, device=dev), torch.empty(n * 64, dtype=torch.uint8, device=dev),
             torch.empty(n * L, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int32, device=dev)]
     vers = [torch.zeros(n // 32, dtype=torch.int32, device=dev) for _ in lstreams]
@@ -448,6 +452,7 @@ def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
     v.close()
     return {"value": n * steps / dt, "unit": "verifies/s", "records_per_step": n, "senders": senders, "steps": steps,
             "ms_per_step": dt * 1e3 / steps, "kernel_ms": kernel_ms, "verdicts_ok": ok,
+            "context_create_s": t_create,
             "cache_chunk_hits": info["cache_chunk_hits"],
             "cache_chunks": info["cache_chunks"],
             "cache_record_hits": info["cache_record_hits"],
@@ -455,11 +460,12 @@ def at2_traffic_leg(args, at2v, torch, dev, lstreams, n, L, senders=64):
                          "achieved": n * steps / dt * COMB_MAC_PER_VERIFY / 1e12, "peak": MAC_PEAK / 1e12,
                          "unit": "Tops/s (32x32->64 integer MAC, v_mad_u64_u32)",
                          "frac": n * steps / dt * COMB_MAC_PER_VERIFY / MAC_PEAK,
-                         "note": "at the wall-clock step rate (launch gaps included); 301 M + 63.5 S per verify "
+                         "note": "at the wall-clock step rate (launch gaps included); 266 M + 63.5 S per verify "
                                  "(affine comb entries; four records per lane share one inversion)"},
             "method": f"{n} records per step (100-byte M) signed by {senders} repeating senders (GPU generator, record i "
                       f"by sender i % {senders}), sender_cache 1024 + sender_comb: chunks whose senders are all cached "
-                      "verify by comb additions (DESIGN §10d); combs built in the warm-up. kernel_ms = device time per "
+                      "verify by comb additions (DESIGN §10d), wide comb of B (AT2V_CTX_BCOMB_WIDE, 24-bit windows); combs built in the "
+                      "warm-up. kernel_ms = device time per "
                       "step on the launch streams (HIP events: the verify kernel and the cache-counter copy; the build "
                       "and flip kernels run on the context's own stream)"}
 

@@ -133,8 +133,10 @@ struct HostComb {
     std::memcpy(&c, w.data() + (size_t)pend[st] * kCombWords, sizeof(CombEntry));
   }
 };
-// D[i][j] = [j 2^(16 i)]B on demand: (j 2^(16 i)) mod l times B by the signed-field base ladder, then the unsigned form
-struct HostBComb {
+// D[i][j] = [j 2^(W i)]B on demand (W = kBCombBits): (j 2^(16 i)) mod l times B by the signed-field base ladder, then the unsigned form
+template <int W>
+struct HostBCombW {
+  static constexpr int kBits = W;
   mutable std::map<uint64_t, gu_niels> t;
   mutable uint64_t pend[2] = {0, 0};
   void prefetch(int st, int i, int j) const { pend[st] = ((uint64_t)i << 32) | (uint32_t)j; }
@@ -144,7 +146,7 @@ struct HostBComb {
       const int i = (int)(pend[st] >> 32);
       const uint32_t j = (uint32_t)pend[st];
       uint32_t x[16] = {0}, k[8];
-      const int bit = 16 * i;
+      const int bit = W * i;
       x[bit >> 5] |= j << (bit & 31);
       if ((bit & 31) && (bit >> 5) + 1 < 16) x[(bit >> 5) + 1] |= (uint32_t)((uint64_t)j >> (32 - (bit & 31)));
       sc_reduce512(k, x);
@@ -183,7 +185,8 @@ int main(int argc, char** argv) {
   // 6: the four-wave kernel's split half-size check for chunks without combs (split_* in at2v_verify_fu.h)
   const int half = argc > 3 ? atoi(argv[3]) : 0;
   std::map<std::vector<uint32_t>, HostComb> combs;
-  HostBComb bcomb;
+  HostBCombW<kBCombBits> bcomb;        // verify_comb_fu (the throughput kernels' comb of B)
+  HostBCombW<kBCombLatBits> bcomb_lat;  // the low-latency kernel's split forms (modes 5 and 6)
   for (size_t i = 0; i < n && (int)i < limit; ++i) {
     uint32_t R[8], A[8], S[8];
     words(R, &sig[64 * i]);
@@ -205,7 +208,7 @@ int main(int argc, char** argv) {
         gu_p3 Ad, P0, P1;
         const int ok0 = split_a_side(Ad, R, A, S, policy, fa);
         const int ok1 = split_r_side(R, fr);
-        uint32_t c0d[8], c1d[8], td[8];
+        uint32_t c0d[8], c1d[8], td[kBCombLatDigitWords];
         int c1_neg, nw;
         const int ok2 = split_scalars(c0d, c1d, td, c1_neg, nw, R, A, S, len, mw);
         nw = nw < 1 ? 1 : nw;  // (the kernel takes the wave maximum; one lane here)
@@ -213,7 +216,7 @@ int main(int argc, char** argv) {
         split_side_ladder(P1, c1d, nw, c1_neg, fr);
         gu_cached c1, ntb;
         gu_p3_to_cached(c1, P1);
-        split_neg_tb(ntb, td, bcomb);
+        split_neg_tb(ntb, td, bcomb_lat);
         return ok0 & ok1 & ok2 & split_combine(P0, c1, ntb);
       };
       d = split(POLICY_DALEK_V1);
@@ -226,10 +229,10 @@ int main(int argc, char** argv) {
       auto split = [&](int policy) {
         gu_p3 Rp, Pb, Pa0, Pa1;
         const int ok0 = comb_decode_r(Rp, R) & comb_prechecks(R, A, S, policy, c.a_ok);
-        uint32_t sd[8], kd[kCombDigitWords];
-        sc_recode16(sd, S);
+        uint32_t sd[kBCombLatDigitWords], kd[kCombDigitWords];
+        bcomb_recode<kBCombLatBits>(sd, S);
         gu_p3_identity(Pb);
-        comb_sum<false>(Pb, sd, 0, kBCombPos, bcomb);
+        comb_sum<false>(Pb, sd, 0, kBCombLatPos, bcomb_lat);
         comb_k_digits(kd, R, A, len, mw);
         gu_p3_identity(Pa0);
         gu_p3_identity(Pa1);

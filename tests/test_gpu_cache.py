@@ -499,7 +499,8 @@ def test_partition_switch_same_verdicts(at2v_mod, golden, monkeypatch, comb, par
             v.info()
 
 
-def test_comb_hits_staged_and_unstaged_messages(at2v_mod, oracle):
+@pytest.mark.parametrize("wide", [False, True], ids=["bcomb16", "bcomb24"])
+def test_comb_hits_staged_and_unstaged_messages(at2v_mod, oracle, wide):
     """The comb hit loop stages a record's message in LDS when every lane's message fits the stage (length up to ~150
     bytes) and ends 8 bytes before the buffer end; any other wave reads word by word (comb2_point_staged returns -1).
     64 cached senders, 4,096 records with message lengths 0..199 at every byte alignment (so some 64-record waves fit
@@ -524,9 +525,27 @@ def test_comb_hits_staged_and_unstaged_messages(at2v_mod, oracle):
             msg[off[i] + rng.integers(0, lens[i])] ^= 0x01
     want = oracle.verify_batch(pk, sig, msg, off)
     assert 0 < want.sum() < n
-    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=True, admit_first=True) as v:
+    with at2v_mod.BatchVerifier(small_batch_max=OFF, sender_cache=1024, sender_comb=True, admit_first=True,
+                                bcomb_wide=wide) as v:
         for rep in range(3):
             got = v.verify_batch(pk, sig, msg, off)
             assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
             info = v.info()
         assert info["cache_record_hits"] >= 2 * n, info
+
+
+@pytest.mark.parametrize("policy", ["dalek", "libsodium"])
+def test_wide_bcomb_golden_sets(at2v_mod, golden, policy):
+    """AT2V_CTX_BCOMB_WIDE: the throughput kernel's cached records take [s]B from the 24-bit-window comb of B (11
+    entries instead of 16). Every golden set, cold then warm (admit_first: the warm pass is all cached), both policies,
+    large launches (the hit-list kernel) and small ones (the low-latency kernel, which keeps the 16-bit comb)."""
+    for small in (OFF, 0):
+        with at2v_mod.BatchVerifier(policy=policy, small_batch_max=small, sender_cache=1 << 14, sender_comb=True,
+                                    admit_first=True, bcomb_wide=True) as v:
+            for name in golden_io.SETS:
+                g = golden[name]
+                want = g.dalek if policy == "dalek" else g.sodium
+                for rep in range(2):
+                    got = v.verify_batch(g.pk, g.sig, g.msg, g.off)
+                    assert np.array_equal(got, want), (small, name, rep, np.nonzero(got != want)[0][:10])
+                    v.info()

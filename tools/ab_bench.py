@@ -20,7 +20,7 @@ class Opts(ctypes.Structure):  # include/at2v.h at2v_opts (ABI v6)
                 ("cpu_threads", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
-def open_lib(path, comb=False):
+def open_lib(path, comb=False, wide=False):
     lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
     P = ctypes.c_void_p
     lib.at2v_create.argtypes = [P, ctypes.POINTER(P)]
@@ -28,7 +28,7 @@ def open_lib(path, comb=False):
     lib.at2v_gen_records_senders_device.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
                                                     ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P]
     h = P()
-    o = Opts(0, 1, 0, 0, 1024 if comb else 0, 1 if comb else 0, 0, 0)
+    o = Opts(0, 1, 0, 0, 1024 if comb else 0, 1 if comb else 0, 0, 4 if (comb and wide) else 0)
     assert lib.at2v_create(ctypes.byref(o), ctypes.byref(h)) == 0
     return lib, h
 
@@ -42,12 +42,13 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="perf-only experiment builds: skip the verdict check")
     ap.add_argument("--senders", type=int, default=0, help="records signed by this many repeating senders (0 = distinct)")
     ap.add_argument("--comb", action="store_true", help="contexts with sender_cache 1024 + sender_comb (AT2 traffic)")
+    ap.add_argument("--wide", action="store_true", help="with --comb: the wide comb of B (AT2V_CTX_BCOMB_WIDE)")
     ap.add_argument("--probe", action="store_true",
                     help="builds with -DAT2V_COMB_PROBE: print the comb kernel's per-wait cycle sums (rounds 2..)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L = a.n, a.msg_len
-    libs = [open_lib(p, a.comb) for p in a.libs]
+    libs = [open_lib(p, a.comb, a.wide) for p in a.libs]
     s = torch.cuda.current_stream()
     d_pk = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     d_sig = torch.empty(n * 64, dtype=torch.uint8, device="cuda")

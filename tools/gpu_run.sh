@@ -26,6 +26,7 @@
 #   stall/stallat2 wave-cycle split (issue / issue-stall / s_waitcnt) of verify_kernel / verify_kernel_comb
 #   icache        tools/icache_pmc.sh: instruction-cache hits / misses of the comb and ladder kernels
 #   abchurn=<a,b> tools/ab_churn.sh: the bench's AT2-traffic and churn legs with variant a / b, alternating, 2 rounds
+#   ab5=<a,b>     tools/ab_config5.sh: config 5 (0% and 2% first-seen senders) with variant a / b, alternating
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
 #   ab=<a,b,...>  tools/ab_bench.py over at2-node_amd/at2v/variants/libat2v_<a>.so ... (distinct keys)
 #   abcomb=<...>  the same on 64-sender traffic with combs
@@ -106,6 +107,7 @@ for st in "$@"; do
     stallat2) run stallat2 400 bash tools/stall_pmc_at2.sh $TAG ;;
     icache) run icache 400 bash tools/icache_pmc.sh $TAG ;;
     abchurn=*) run abchurn 900 bash tools/ab_churn.sh $TAG $(echo "${st#abchurn=}" | tr ',' ' ') 2 ;;
+    ab5=*) run ab5 900 bash tools/ab_config5.sh $TAG $(echo "${st#ab5=}" | tr ',' ' ') 1 ;;
     stall) run stall 300 bash tools/stall_pmc_quick.sh $TAG ;;
     latency) run latency 400 python3 tools/latency_probe.py --reps 100 --comb 1
              grep '^{' $D/latency.txt > $D/latency_comb1.json ;;
