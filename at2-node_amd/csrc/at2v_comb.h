@@ -45,13 +45,13 @@ static_assert((kCombPos << kCombWideLog2) <= 256, "one 256-thread block builds a
 static_assert((kCombPos << kCombNarrowLog2) <= 64, "one wave builds a key's comb");
 constexpr int kCombWideMaxKeys = 256;  // new keys per launch up to which the wide builder runs (1,024 waves)
 constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
-// The comb of B (one per context): signed radix-2^W digits of s, W = AT2V_BCOMB_BITS. W = 24 (default since round 5):
-// 11 positions x (2^23 + 1) entries, 11.8 GB of the 288 GB HBM, five additions fewer per record than W = 16 (16 positions
-// x (2^15 + 1) entries, 67 MB); W = 20: 13 positions, 872 MB. 64-sender traffic: 514.0 / 535.4 / 551.8 M/s for W = 16 /
-// 20 / 24 (profiles/r05v/abcomb.txt).
-// The low-latency kernel (one wave per part of a record, every access on its critical path) keeps reading a W = 16 comb
-// of B that stays in the MALL: its 64 lanes' random entries in an 11.8 GB table cost a page walk each (config 5's queue
-// p50 went from 0.15 to 0.43 ms with W = 24 there, profiles/r05w). A context with combs holds both tables.
+// The comb of B: signed radix-2^W digits of s. Every context with combs holds a W = 16 table (16 positions x (2^15 + 1)
+// entries, 67 MB, MALL-resident), read by every comb path. AT2V_CTX_BCOMB_WIDE adds a W = AT2V_BCOMB_BITS table for the
+// hit-list kernel: W = 24, 11 positions x (2^23 + 1) entries, 11.8 GB of the 288 GB HBM, five additions fewer per record
+// (W = 20: 13 positions, 872 MB). 64-sender traffic: 514.0 / 535.4 / 551.8 M/s for W = 16 / 20 / 24
+// (profiles/r05v/abcomb_bcomb_bits.txt). Not the default: with the wide table in each node process of the config-5
+// mini-network (an eager queue whose small launches never read it), queue p50 with first-seen senders rose from 0.15
+// to 0.43 ms and p99 to tens of ms (profiles/r05y, r05w).
 #ifndef AT2V_BCOMB_BITS
 #define AT2V_BCOMB_BITS 24
 #endif
@@ -63,8 +63,8 @@ struct BCombGeom {
   static constexpr int kDigitWords = W == 16 ? 8 : kPos;        // 16: two halfword digits per word
   static constexpr size_t kBytes = (size_t)kPos * kEntries * 128;
 };
-constexpr int kBCombBits = AT2V_BCOMB_BITS;  // the throughput kernels' comb of B
-constexpr int kBCombLatBits = 16;            // the low-latency kernel's
+constexpr int kBCombBits = AT2V_BCOMB_BITS;  // the wide comb of B (AT2V_CTX_BCOMB_WIDE)
+constexpr int kBCombLatBits = 16;            // every comb context's comb of B
 constexpr int kBCombPos = BCombGeom<kBCombBits>::kPos;
 constexpr int kBCombEntries = BCombGeom<kBCombBits>::kEntries;
 constexpr int kBCombDigitWords = BCombGeom<kBCombBits>::kDigitWords;
