@@ -29,7 +29,7 @@
 #   ab5=<a,b>     tools/ab_config5.sh: config 5 (0% and 2% first-seen senders) with variant a / b, alternating
 #   pmc           tools/profile.sh: rocprofv3 kernel trace + the PMC passes (one counter group per pass)
 #   ab=<a,b,...>  tools/ab_bench.py over at2-node_amd/at2v/variants/libat2v_<a>.so ... (distinct keys)
-#   abcomb=<...>  the same on 64-sender traffic with combs
+#   abcomb=<...>  the same on 64-sender traffic with combs (abwide=: with the wide comb of B, AT2V_CTX_BCOMB_WIDE)
 #   cprobe=<...>  the same with --probe: per-wait cycle table of builds made with -DAT2V_COMB_PROBE (cprobex=: without
 #                 the verdict check, for timing-only experiment builds)
 set -o pipefail
@@ -123,6 +123,9 @@ for st in "$@"; do
     cprobe=*|cprobex=*) libs=""; chk=""; [ "${st%%=*}" = cprobex ] && chk="--no-check"
           for v in $(echo "${st#*=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
           run ${st%%=*} 900 python3 tools/ab_bench.py $libs --rounds 8 --senders 64 --comb --probe $chk ;;
+    abwide=*) libs=""  # AT2 traffic through contexts with the wide comb of B
+          for v in $(echo "${st#abwide=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
+          run abwide 900 python3 tools/ab_bench.py $libs --rounds 12 --senders 64 --comb --wide ;;
     abcombx=*) libs=""  # experiment builds (wrong verdicts allowed)
           for v in $(echo "${st#abcombx=}" | tr ',' ' '); do libs="$libs at2-node_amd/at2v/variants/libat2v_$v.so"; done
           run abcombx 900 python3 tools/ab_bench.py $libs --rounds 12 --senders 64 --comb --no-check ;;
