@@ -219,10 +219,10 @@ class BatchVerifier:
         """small_batch_max: launches of at most this many records run the low-latency kernel (two lanes per record);
         0 = the library default (SMALL_BATCH_DEFAULT), SMALL_BATCH_OFF = always the throughput kernel.
         sender_cache: capacity of the per-sender A cache in distinct public keys (0 = off).
-        sender_comb: with sender_cache, also keep a comb of -A per cached key (1.7 MB of HBM each, plus one 67 MB comb
-        of B per context; include/at2v.h): records whose sender is cached verify by table additions only (at2v_comb.h),
-        launches of every size. bcomb_wide: with sender_comb, also an 11.8 GB comb of B with 24-bit windows for the
-        throughput kernel (five additions fewer per cached record; AT2V_CTX_BCOMB_WIDE).
+        sender_comb: with sender_cache, also keep a comb of -A per cached key (1.7 MB of HBM each, plus combs of B of 67
+        MB and 872 MB per context; include/at2v.h): records whose sender is cached verify by table additions only
+        (at2v_comb.h), launches of every size. bcomb_wide: with sender_comb, the throughput kernel's comb of B gets 24-bit
+        windows (11.8 GB, two additions fewer per cached record; AT2V_CTX_BCOMB_WIDE).
         num_gpus=0: the CPU batch backend (no device; cpu_threads host threads, 0 = every usable CPU).
         cpu_fallback: a GPU context re-runs a host-buffer batch on the CPU backend after a device error (same verdicts;
         info()["cpu_fallbacks"] counts it). admit_first: cache keys claim a payload at their first sighting."""

@@ -263,17 +263,17 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit
   a.ctl = (unsigned long long*)c->ctl.p;
   a.seen = (unsigned long long*)c->seen.p;
   a.new_list = (uint4*)c->claim_list[0].p;
-  if (comb) {  // the comb of B (16-bit windows) and, with AT2V_CTX_BCOMB_WIDE, the wide one; built once
-    AT2V_TRY(c->bcomb_lat.ensure(at2v::bcomb_bytes(1)));
-    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb_lat.p, 1, s.stream));
-    a.bcomb = a.bcomb_lat = (const int4*)c->bcomb_lat.p;
-    a.bcomb_wide = 0;
-    if (bcomb_wide && at2v::bcomb_bits(0) != at2v::bcomb_bits(1)) {
-      AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes(0)));
-      AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, 0, s.stream));
-      a.bcomb = (const int4*)c->bcomb.p;
-      a.bcomb_wide = 1;
-    }
+  if (comb) {  // the combs of B, built once: 16-bit windows (low-latency kernel and every other comb path) and 20-bit
+               // ones for the hit-list kernel, 24-bit with AT2V_CTX_BCOMB_WIDE
+    const int lat_bits = at2v::bcomb_lat_bits();
+    const int bits = bcomb_wide ? at2v::bcomb_wide_bits() : at2v::bcomb_mid_bits();
+    AT2V_TRY(c->bcomb_lat.ensure(at2v::bcomb_bytes(lat_bits)));
+    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb_lat.p, lat_bits, s.stream));
+    AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes(bits)));
+    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, bits, s.stream));
+    a.bcomb_lat = (const int4*)c->bcomb_lat.p;
+    a.bcomb = (const int4*)c->bcomb.p;
+    a.bcomb_bits = bits;
   }
   AT2V_TRY(at2v::launch_cache_init(a, s.stream));
   AT2V_TRY(hipStreamSynchronize(s.stream));
@@ -507,11 +507,14 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   std::random_device rd;
+  // test hook (A/B runs of processes the caller does not configure, e.g. the config-5 mini-network's nodes)
+  const char* wide_v = std::getenv("AT2V_BCOMB_WIDE");
+  const bool wide_env = wide_v && std::atoi(wide_v) != 0;
   for (int g = 0; g < o.num_gpus; ++g) {
     int rc = init_shard(c->shards[(size_t)g], alias ? (o.device + g) % ndev : o.device + g);
     if (rc == AT2V_OK && o.sender_cache)
       rc = init_cache(c->shards[(size_t)g], o.sender_cache, ((uint64_t)rd() << 32) ^ rd(), o.sender_comb != 0,
-                      (o.flags & AT2V_CTX_ADMIT_FIRST) != 0, (o.flags & AT2V_CTX_BCOMB_WIDE) != 0);
+                      (o.flags & AT2V_CTX_ADMIT_FIRST) != 0, (o.flags & AT2V_CTX_BCOMB_WIDE) != 0 || wide_env);
     // the cross-rank failure flag of at2v_comm_init_rank / at2v_verify_batch_sharded (first device): allocated here,
     // so a rank whose communicator set-up fails can still join the outcome all-reduce
     if (rc == AT2V_OK && g == 0) rc = hip_code(c->status.ensure(4));

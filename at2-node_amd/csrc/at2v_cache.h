@@ -37,9 +37,9 @@ struct CacheArgs {
   uint32_t epoch;            // launch number (entries record the last one that used them)
   int comb;                  // 1: payloads are combs of -A (sender_comb), 0: tables [j]A
   const int4* bcomb_lat;     // sender_comb: the comb of B, 16-bit windows (kBCombLatBits; 67 MB, MALL-resident)
-  const int4* bcomb;         // AT2V_CTX_BCOMB_WIDE: the wide comb of B (kBCombBits-bit windows, 11.8 GB), read by the
-                             // hit-list kernel only; otherwise = bcomb_lat
-  int bcomb_wide;            // 1: bcomb is the wide table
+  const int4* bcomb;         // sender_comb: the hit-list kernel's comb of B: kBCombMidBits-bit windows (872 MB), or
+                             // with AT2V_CTX_BCOMB_WIDE kBCombBits-bit ones (11.8 GB)
+  int bcomb_bits;            // bcomb's window (20 or 24)
   unsigned long long* ctl;   // counters, kCtl* in at2v_kernels.hip
   uint64_t seed;             // fingerprint key (random per context)
   uint64_t fp_mask;          // fingerprint bits kept (all in the product; fewer in a test that forces collisions)
@@ -78,9 +78,11 @@ struct CacheCompactArgs {
 
 size_t cache_entry_bytes();
 size_t cache_payload_bytes(int comb);  // one key's payload: table [j]A or comb
-size_t bcomb_bytes(int lat);           // the comb of B (lat: the low-latency kernel's)
-int bcomb_bits(int lat);
-hipError_t launch_build_bcomb(int4* out, int lat, hipStream_t stream);
+size_t bcomb_bytes(int bits);          // a comb of B with bits-bit windows (16, 20 or 24)
+int bcomb_lat_bits();
+int bcomb_mid_bits();
+int bcomb_wide_bits();
+hipError_t launch_build_bcomb(int4* out, int bits, hipStream_t stream);
 int cache_ctl_words();
 // ctl word indices the host reads (at2v_get_info) and resets
 enum CacheCtlWord : int {

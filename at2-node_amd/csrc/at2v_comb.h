@@ -45,13 +45,14 @@ static_assert((kCombPos << kCombWideLog2) <= 256, "one 256-thread block builds a
 static_assert((kCombPos << kCombNarrowLog2) <= 64, "one wave builds a key's comb");
 constexpr int kCombWideMaxKeys = 256;  // new keys per launch up to which the wide builder runs (1,024 waves)
 constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
-// The comb of B: signed radix-2^W digits of s. Every context with combs holds a W = 16 table (16 positions x (2^15 + 1)
-// entries, 67 MB, MALL-resident), read by every comb path. AT2V_CTX_BCOMB_WIDE adds a W = AT2V_BCOMB_BITS table for the
-// hit-list kernel: W = 24, 11 positions x (2^23 + 1) entries, 11.8 GB of the 288 GB HBM, five additions fewer per record
-// (W = 20: 13 positions, 872 MB). 64-sender traffic: 514.0 / 535.4 / 551.8 M/s for W = 16 / 20 / 24
-// (profiles/r05v/abcomb_bcomb_bits.txt). Not the default: with the wide table in each node process of the config-5
-// mini-network (an eager queue whose small launches never read it), queue p50 with first-seen senders rose from 0.15
-// to 0.43 ms and p99 to tens of ms (profiles/r05y, r05w).
+// The combs of B: signed radix-2^W digits of s. Every context with combs holds two: W = 16 (16 positions x (2^15 + 1)
+// entries, 67 MB, MALL-resident), read by the low-latency kernel and every other comb path, and W = 20 (13 positions,
+// 872 MB) for the hit-list kernel, three additions fewer per record. AT2V_CTX_BCOMB_WIDE makes the latter W = 24 (11
+// positions x (2^23 + 1) entries, 11.8 GB of the 288 GB HBM, five fewer). 64-sender traffic: 514.0 / 535.4 / 551.8 M/s
+// with W = 16 / 20 / 24 in the hit-list kernel (profiles/r05v/abcomb_bcomb_bits.txt). W = 24 is opt-in: with it in each
+// node process of the config-5 mini-network (an eager queue whose small launches never read it), queue p50 with
+// first-seen senders rose from 0.15 to 0.43 ms and p99 to tens of ms; W = 20 there left both unchanged (profiles/r05y,
+// r05zc).
 #ifndef AT2V_BCOMB_BITS
 #define AT2V_BCOMB_BITS 24
 #endif
@@ -64,7 +65,8 @@ struct BCombGeom {
   static constexpr size_t kBytes = (size_t)kPos * kEntries * 128;
 };
 constexpr int kBCombBits = AT2V_BCOMB_BITS;  // the wide comb of B (AT2V_CTX_BCOMB_WIDE)
-constexpr int kBCombLatBits = 16;            // every comb context's comb of B
+constexpr int kBCombMidBits = 20;            // every comb context's throughput comb of B (872 MB)
+constexpr int kBCombLatBits = 16;            // every comb context's low-latency comb of B (67 MB)
 constexpr int kBCombPos = BCombGeom<kBCombBits>::kPos;
 constexpr int kBCombEntries = BCombGeom<kBCombBits>::kEntries;
 constexpr int kBCombDigitWords = BCombGeom<kBCombBits>::kDigitWords;

@@ -446,7 +446,6 @@ struct DevBCombW {
     }
   }
 };
-using DevBCombWide = DevBCombW<kBCombBits>;    // AT2V_CTX_BCOMB_WIDE contexts' comb of B (the hit-list kernel)
 using DevBCombLat = DevBCombW<kBCombLatBits>;  // every context with combs (all other comb paths)
 
 __device__ AT2V_INLINE void stage_btab(int4* lds) {
@@ -1989,9 +1988,12 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   (void)btab;
   const uint32_t nh = __builtin_amdgcn_readfirstlane(p.counts[0]);
-  if (c.bcomb_wide)
+  if (c.bcomb_bits == kBCombBits)
     verify_comb_hits<4, kBCombBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
                                     chunk_queue, c, p, nh);
+  else if (c.bcomb_bits == kBCombMidBits)
+    verify_comb_hits<4, kBCombMidBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+                                       chunk_queue, c, p, nh);
   else if (AT2V_COMB_HITS8 && nh > 256u * gridDim.x * kWavesPerBlock)
     verify_comb_hits<8, kBCombLatBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
                                        chunk_queue, c, p, nh);
@@ -2627,11 +2629,15 @@ __global__ __launch_bounds__(kBlock) void build_bcomb_kernel(int4* __restrict__ 
 
 size_t cache_entry_bytes() { return (size_t)kCacheEntryGranules * 16; }
 size_t cache_payload_bytes(int comb) { return comb ? kCombBytes : (size_t)kTabAGranules * 16; }
-size_t bcomb_bytes(int lat) { return lat ? BCombGeom<kBCombLatBits>::kBytes : BCombGeom<kBCombBits>::kBytes; }
-int bcomb_bits(int lat) { return lat ? kBCombLatBits : kBCombBits; }
+size_t bcomb_bytes(int bits) {
+  return bits == 24 ? BCombGeom<24>::kBytes : bits == 20 ? BCombGeom<20>::kBytes : BCombGeom<16>::kBytes;
+}
+int bcomb_lat_bits() { return kBCombLatBits; }
+int bcomb_mid_bits() { return kBCombMidBits; }
+int bcomb_wide_bits() { return kBCombBits; }
 
-hipError_t launch_build_bcomb(int4* out, int lat, hipStream_t stream) {
-  const int bits = bcomb_bits(lat), npos = (254 + bits - 1) / bits;
+hipError_t launch_build_bcomb(int4* out, int bits, hipStream_t stream) {
+  const int npos = (254 + bits - 1) / bits;
   const uint32_t entries = (1u << (bits - 1)) + 1;
   for (int pos = 0; pos < npos; ++pos) {
     hipLaunchKernelGGL(build_bcomb_kernel, dim3((entries + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out, bits,

@@ -99,7 +99,7 @@ impl Default for At2vOpts {
 pub const AT2V_CTX_CPU_FALLBACK: u32 = 1;
 /// `At2vOpts::flags`: sender-cache keys claim a payload at their first sighting (default: the second).
 pub const AT2V_CTX_ADMIT_FIRST: u32 = 2;
-/// `At2vOpts::flags`: with sender_comb, also an 11.8 GB comb of B (24-bit windows) for the throughput kernel.
+/// `At2vOpts::flags`: with sender_comb, the throughput kernel's comb of B with 24-bit windows (11.8 GB, default 20-bit).
 pub const AT2V_CTX_BCOMB_WIDE: u32 = 4;
 
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;

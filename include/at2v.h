@@ -62,9 +62,9 @@ typedef struct {
                                stream after that launch and serves later launches. When the capacity is reached, the
                                least recently used entries (by launch) are replaced; up to 3/4 of the capacity stays. */
   uint32_t sender_comb;     /* with sender_cache: 1 = every cached key also gets a comb of -A ([j 2^(10i)](-A), 1.7 MB
-                               per key, sender_cache x 1.7 MB per device, plus a 67 MB comb of B per context;
-                               AT2V_CTX_BCOMB_WIDE adds a wider one), and a record whose sender is cached is verified by
-                               42 table additions (37 with the wide comb of B) and one
+                               per key, sender_cache x 1.7 MB per device, plus combs of B of 67 MB and 872 MB per context;
+                               AT2V_CTX_BCOMB_WIDE widens the second), and a record whose sender is cached is verified by
+                               39 table additions (37 with the wide comb of B) and one
                                inversion instead of the doubling ladder (~3x fewer multiplications; launches of any size,
                                small batches included). Same verdicts. 0 = off. */
   uint32_t cpu_threads;     /* host threads of the CPU backend (num_gpus = 0, or AT2V_CTX_CPU_FALLBACK): 0 = every CPU
@@ -79,10 +79,11 @@ typedef struct {
  * again in a later launch, or when one wave of a launch holds two or more of its records, so one-shot senders cost a
  * sighting (one 8-byte store) instead of a build. This flag admits every key at its first sighting (round-4 behaviour). */
 #define AT2V_CTX_ADMIT_FIRST 2u
-/* With sender_comb: also keep a wide comb of B (24-bit windows, 11 positions, 11.8 GB of HBM per device) that the
- * throughput kernel's cached records read: five table additions fewer per record (37 instead of 42), +7% on repeating
- * senders (a context with it took 0.76 s to create). For throughput-bound contexts: with it in every node process of the
- * config-5 mini-network (an eager queue, first-seen senders), queue p50 rose from 0.15 to 0.43 ms. */
+/* With sender_comb: the throughput kernel's cached records take [s]B from a comb of B with 24-bit windows (11 positions,
+ * 11.8 GB of HBM per device) instead of the default 20-bit one (13 positions, 872 MB): two table additions fewer per
+ * record (37 instead of 39), +3% on repeating senders (a context with it took 0.76 s to create). For throughput-bound
+ * contexts: with it in every node process of the config-5 mini-network (an eager queue, first-seen senders), queue p50
+ * rose from 0.15 to 0.43 ms; the 20-bit table left it unchanged. */
 #define AT2V_CTX_BCOMB_WIDE 4u
 #define AT2V_SMALL_BATCH_DEFAULT 32768u
 #define AT2V_SMALL_BATCH_OFF 0xffffffffu
