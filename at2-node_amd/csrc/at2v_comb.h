@@ -43,7 +43,14 @@ constexpr int kCombWideLog2 = 3, kCombNarrowLog2 = 1;
 static_assert(kCombBits - 1 - kCombWideLog2 >= 1, "comb builder parts");
 static_assert((kCombPos << kCombWideLog2) <= 256, "one 256-thread block builds a key's comb");
 static_assert((kCombPos << kCombNarrowLog2) <= 64, "one wave builds a key's comb");
-constexpr int kCombWideMaxKeys = 256;  // new keys per launch up to which the wide builder runs (1,024 waves)
+// new keys per launch up to which the wide builder runs (a 256-thread block per key). A build block holds its CU for
+// the ~1 ms of a comb's 250-doubling position chain, and no verify block fits beside it (they take the whole register
+// file), so AT2V_COMB_WIDE_MAX bounds the CUs builds take from the verify kernels: above it, one wave per key (four keys
+// per block).
+#ifndef AT2V_COMB_WIDE_MAX
+#define AT2V_COMB_WIDE_MAX 8  // 256 (a block per key up to 256 keys): Zipf / 4x-capacity legs 2-3% slower (profiles/r05zf)
+#endif
+constexpr int kCombWideMaxKeys = AT2V_COMB_WIDE_MAX;
 constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, two 16-bit fields per word
 // The combs of B: signed radix-2^W digits of s. Every context with combs holds two: W = 16 (16 positions x (2^15 + 1)
 // entries, 67 MB, MALL-resident), read by the low-latency kernel and every other comb path, and W = 20 (13 positions,

@@ -2663,6 +2663,7 @@ hipError_t launch_cache_build(const CacheArgs& c, uint32_t max_claims, hipStream
   if (max_claims == 0) max_claims = 1;
   if (c.comb) {  // a block per claim (few claims) or a wave per claim; the grid loops over more
     hipLaunchKernelGGL(cache_comb_kernel, dim3(max_claims < 512u ? max_claims : 512u), dim3(256), 0, stream, c);
+    // (the kernel reads the real claim count: blocks past the keys' blocks (wide) or waves (narrow) exit at once)
   } else {
     hipLaunchKernelGGL(cache_build_kernel, dim3(grid_for(max_claims, 256, 1024)), dim3(256), 0, stream, c);
   }
