@@ -1972,13 +1972,9 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
 #endif
 }
 
-// partitioned cached launches: the classify kernel's hit list by comb additions, four records per lane. AT2V_COMB_HITS8
-// = 1 runs eight per lane (one inversion for eight) once the list fills every wave with at least two four-record
-// chunks: 1.4% slower on 1M records from 64 senders (one 512-record chunk per wave leaves the chunk queue nothing to
-// balance).
-#ifndef AT2V_COMB_HITS8
-#define AT2V_COMB_HITS8 0  // 1 measured 1.4% slower on 1M records from 64 senders (profiles/r05n/abcomb.txt)
-#endif
+// partitioned cached launches: the classify kernel's hit list by comb additions, four records per lane (eight per lane,
+// one inversion for eight, measured 1.4% slower on 1M records from 64 senders: one 512-record chunk per wave leaves
+// the chunk queue nothing to balance, profiles/r05n/abcomb.txt), [s]B from the context's 20-bit or 24-bit comb of B
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_comb_part(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
@@ -1988,17 +1984,11 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   (void)btab;
   const uint32_t nh = __builtin_amdgcn_readfirstlane(p.counts[0]);
-  if (c.bcomb_bits == kBCombBits)
+  if (c.bcomb_bits == kBCombBits)  // AT2V_CTX_BCOMB_WIDE
     verify_comb_hits<4, kBCombBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
                                     chunk_queue, c, p, nh);
-  else if (c.bcomb_bits == kBCombMidBits)
-    verify_comb_hits<4, kBCombMidBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
-                                       chunk_queue, c, p, nh);
-  else if (AT2V_COMB_HITS8 && nh > 256u * gridDim.x * kWavesPerBlock)
-    verify_comb_hits<8, kBCombLatBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
-                                       chunk_queue, c, p, nh);
   else
-    verify_comb_hits<4, kBCombLatBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+    verify_comb_hits<4, kBCombMidBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
                                        chunk_queue, c, p, nh);
 }
 
