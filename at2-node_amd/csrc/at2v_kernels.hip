@@ -984,18 +984,25 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 // and adds its statistics with one atomic per counter. (One wave per group with per-wave atomics took 0.54-0.77 ms per
 // 1M records: ~100k atomics on a handful of control words, profiles/r05f. Eight groups per wave and per-wave list
 // atomics: the same atomic count as now, but each wave ran eight dependent lookup chains one after the other.)
+// Block shape: AT2V_CLASSIFY_WAVES waves x AT2V_CLASSIFY_GROUPS groups. Blocks of 16 waves x 4 groups (8x fewer list and
+// statistics atomics on the same control words) measured no better on the distinct-key leg (0.977 against 0.982-0.987
+// of plain, profiles/r05zi): the atomics are not what the classify kernel waits for.
 #ifndef AT2V_CLASSIFY_GROUPS
 #define AT2V_CLASSIFY_GROUPS 2
 #endif
+#ifndef AT2V_CLASSIFY_WAVES
+#define AT2V_CLASSIFY_WAVES 4
+#endif
 constexpr int kClassifyGroups = AT2V_CLASSIFY_GROUPS;
-__global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __restrict__ pk, uint32_t n, CacheArgs c,
-                                                             PartArgs p) {
-  __shared__ uint32_t sstat[4][8];
+constexpr int kClassifyWaves = AT2V_CLASSIFY_WAVES;
+__global__ __launch_bounds__(64 * AT2V_CLASSIFY_WAVES) void cache_classify_kernel(const uint8_t* __restrict__ pk,
+                                                                                 uint32_t n, CacheArgs c, PartArgs p) {
+  __shared__ uint32_t sstat[kClassifyWaves][8];
   __shared__ uint32_t sbase[2];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const uint32_t ngroups = (n + 63) / 64;
-  const uint32_t g0 = (blockIdx.x * 4 + (uint32_t)wib) * kClassifyGroups;
+  const uint32_t g0 = (blockIdx.x * kClassifyWaves + (uint32_t)wib) * kClassifyGroups;
   LookupStats st;
   uint64_t hm[kClassifyGroups], am[kClassifyGroups];
   uint32_t info[kClassifyGroups];
@@ -1033,13 +1040,17 @@ __global__ __launch_bounds__(256) void cache_classify_kernel(const uint8_t* __re
   }
   __syncthreads();
   if (threadIdx.x == 0) {  // the block's room in the two lists
-    const uint32_t th = sstat[0][2] + sstat[1][2] + sstat[2][2] + sstat[3][2];
-    const uint32_t tm = sstat[0][7] + sstat[1][7] + sstat[2][7] + sstat[3][7];
+    uint32_t th = 0, tm = 0;
+    for (int w = 0; w < kClassifyWaves; ++w) {
+      th += sstat[w][2];
+      tm += sstat[w][7];
+    }
     sbase[0] = th ? atomicAdd(p.counts, th) : 0u;
     sbase[1] = tm ? atomicAdd(p.counts + 1, tm) : 0u;
   }
   if (threadIdx.x < 7) {
-    const uint32_t v = sstat[0][threadIdx.x] + sstat[1][threadIdx.x] + sstat[2][threadIdx.x] + sstat[3][threadIdx.x];
+    uint32_t v = 0;
+    for (int w = 0; w < kClassifyWaves; ++w) v += sstat[w][threadIdx.x];
     const int k = threadIdx.x;
     const int word = k == 0 ? kCtlChunks : k == 1 ? kCtlChunkHits : k == 2 ? kCtlRecHits : k == 3 ? kCtlFound
                      : k == 4 ? kCtlClaimed : k == 5 ? kCtlFailed : kCtlSighted;
@@ -2742,9 +2753,9 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
     pa.counts = queue + 4;
     hipError_t e = hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    const uint32_t groups = (n + 63) / 64, per_block = 4 * kClassifyGroups;
-    hipLaunchKernelGGL(cache_classify_kernel, dim3((groups + per_block - 1) / per_block), dim3(256), 0, stream, pk, n,
-                       *cache, pa);
+    const uint32_t groups = (n + 63) / 64, per_block = kClassifyWaves * kClassifyGroups;
+    hipLaunchKernelGGL(cache_classify_kernel, dim3((groups + per_block - 1) / per_block), dim3(64 * kClassifyWaves), 0,
+                       stream, pk, n, *cache, pa);
     if (cache->comb) {
       const uint32_t need2 = ((n + 255) / 256 + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);
       const int g2 = (int)((uint32_t)grid < need2 ? (uint32_t)grid : need2);
