@@ -482,7 +482,7 @@ def churn_legs(args, at2v, torch, dev, lstreams, n, L, plain_kernel_ms, plain_va
     charged to the leg. Per leg: wall-clock rate, device time of the launch streams, chunk hit rate, claims, builds
     and their device time, compactions, sightings; vs_plain = this leg's rate over the headline's (distinct keys,
     no cache)."""
-    steps, warm = max(2, args.steps), 3
+    steps, warm = max(2, args.steps), 6  # (six warm-up batches: admission, builds and a compaction reach steady state)
     nb = steps + warm
     gen = torch.Generator(device=dev)
     gen.manual_seed(0x5EED)
