@@ -270,7 +270,9 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit
     AT2V_TRY(c->bcomb_lat.ensure(at2v::bcomb_bytes(lat_bits)));
     AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb_lat.p, lat_bits, s.stream));
     AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes(bits)));
+#if !AT2V_EXP_BCOMB_NOBUILD  // EXPERIMENT (wrong verdicts on the hit path): the table allocated but never written
     AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, bits, s.stream));
+#endif
     a.bcomb_lat = (const int4*)c->bcomb_lat.p;
     a.bcomb = (const int4*)c->bcomb.p;
     a.bcomb_bits = bits;
