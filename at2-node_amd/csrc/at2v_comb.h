@@ -56,10 +56,8 @@ constexpr int kCombDigitWords = (kCombPos + 1) / 2;             // k's digits, t
 // entries, 67 MB, MALL-resident), read by the low-latency kernel and every other comb path, and W = 20 (13 positions,
 // 872 MB) for the hit-list kernel, three additions fewer per record. AT2V_CTX_BCOMB_WIDE makes the latter W = 24 (11
 // positions x (2^23 + 1) entries, 11.8 GB of the 288 GB HBM, five fewer). 64-sender traffic: 514.0 / 535.4 / 551.8 M/s
-// with W = 16 / 20 / 24 in the hit-list kernel (profiles/r05v/abcomb_bcomb_bits.txt). W = 24 is opt-in: with it in each
-// node process of the config-5 mini-network (an eager queue whose small launches never read it), queue p50 with
-// first-seen senders rose from 0.15 to 0.43 ms and p99 to tens of ms; W = 20 there left both unchanged (profiles/r05y,
-// r05zc).
+// with W = 16 / 20 / 24 in the hit-list kernel (profiles/r05v/abcomb_bcomb_bits.txt). W = 24 is opt-in for its memory
+// and its 0.75 s build; config 5's latency is the same with it in every node process (profiles/r05zn).
 #ifndef AT2V_BCOMB_BITS
 #define AT2V_BCOMB_BITS 24
 #endif

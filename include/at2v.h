@@ -81,9 +81,8 @@ typedef struct {
 #define AT2V_CTX_ADMIT_FIRST 2u
 /* With sender_comb: the throughput kernel's cached records take [s]B from a comb of B with 24-bit windows (11 positions,
  * 11.8 GB of HBM per device) instead of the default 20-bit one (13 positions, 872 MB): two table additions fewer per
- * record (37 instead of 39), +3% on repeating senders (a context with it took 0.76 s to create). For throughput-bound
- * contexts: with it in every node process of the config-5 mini-network (an eager queue, first-seen senders), queue p50
- * rose from 0.15 to 0.43 ms; the 20-bit table left it unchanged. */
+ * record (37 instead of 39), +3% on repeating senders. Opt-in for its memory and its 0.75 s of table build at context
+ * creation; small-batch latency is unchanged with it. */
 #define AT2V_CTX_BCOMB_WIDE 4u
 #define AT2V_SMALL_BATCH_DEFAULT 32768u
 #define AT2V_SMALL_BATCH_OFF 0xffffffffu

@@ -32,13 +32,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "at2-node_amd"))
 
 
-def node_main(idx, inboxes, result_q, args, total):
+def node_main(idx, inboxes, result_q, args, total, node_ready=None):
     import numpy as np
 
     from at2v.node import VERDICT_FAILED, IngestQueue, Ledger, SendAssetRequest, pack_send_asset, verdict_mask
 
     q = IngestQueue(device=0, max_batch=args.batch, max_delay_us=args.delay_us, max_msg_bytes=48, depth=3,
                     eager=args.eager, sender_comb=bool(args.comb), sender_cache=args.cache)
+    if node_ready is not None:  # the context (and its tables) is built: traffic may start
+        node_ready.put(idx)
     led = Ledger()
     lock = threading.Lock()
     chunks = []  # submitted runs, ticket order: [first, pk, seq, rcp, amt, t_arrival]
@@ -293,7 +295,9 @@ def main():
             if time.time() > deadline:
                 raise SystemExit("mininode: client did not get ready in 600 s")
     KEYS[:] = info["keys"]
-    nodes = [ctx.Process(target=node_main_with_keys, args=(i, inboxes, result_q, args, info["keys"], info["total"]))
+    node_ready = ctx.Queue()
+    nodes = [ctx.Process(target=node_main_with_keys,
+                         args=(i, inboxes, result_q, args, info["keys"], info["total"], node_ready))
              for i in range(args.nodes)]
     saved = os.environ.get("GPU_MAX_HW_QUEUES")
     if args.node_hw_queues > 0:  # (spawned children take the parent's environment at start)
@@ -305,7 +309,21 @@ def main():
             del os.environ["GPU_MAX_HW_QUEUES"]
         else:
             os.environ["GPU_MAX_HW_QUEUES"] = saved
-    time.sleep(3.0)  # contexts up (first HIP init per process)
+    # every node's queue (context, B tables, combs of B) is built before the client sends: a node still building its
+    # tables would otherwise share the GPU with the others' first batches (a fixed 3 s sleep was too short for the
+    # 11.8 GB comb of B, profiles/r05zm)
+    up, deadline = 0, time.time() + 600
+    while up < args.nodes:
+        try:
+            node_ready.get(timeout=5)
+            up += 1
+        except queue_mod.Empty:
+            dead = [p.exitcode for p in nodes if not p.is_alive()]
+            if dead:
+                raise SystemExit(f"mininode: a node process exited with {dead[0]} before the run started")
+            if time.time() > deadline:
+                raise SystemExit("mininode: nodes did not get ready in 600 s")
+    time.sleep(0.5)
     t0 = time.perf_counter()
     ready_q.put("go")
     offered = ready_q.get(timeout=600)
@@ -333,9 +351,9 @@ def main():
     return 0 if ok else 1
 
 
-def node_main_with_keys(idx, inboxes, result_q, args, keys, total):
+def node_main_with_keys(idx, inboxes, result_q, args, keys, total, node_ready=None):
     KEYS[:] = keys
-    node_main(idx, inboxes, result_q, args, total)
+    node_main(idx, inboxes, result_q, args, total, node_ready)
 
 
 if __name__ == "__main__":
