@@ -53,7 +53,7 @@ class VerifyError(Exception):
     """Signature rejected (drop::crypto::sign::VerifyError)."""
 
 
-ABI_VERSION = 6  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
+ABI_VERSION = 7  # include/at2v.h AT2V_ABI_VERSION: the struct layouts below are those of this version
 E_PEER = -7      # AT2V_E_PEER: another rank of the communicator failed this collective batch
 
 
@@ -82,7 +82,8 @@ class _Info(ctypes.Structure):
                 ("cache_compactions", ctypes.c_uint64), ("cpu_threads", ctypes.c_uint64),
                 ("cpu_batches", ctypes.c_uint64), ("cpu_fallbacks", ctypes.c_uint64),
                 ("cache_sightings", ctypes.c_uint64), ("cache_built", ctypes.c_uint64),
-                ("cache_build_us", ctypes.c_uint64), ("cache_record_hits", ctypes.c_uint64)]
+                ("cache_build_us", ctypes.c_uint64), ("cache_record_hits", ctypes.c_uint64),
+                ("experiments", ctypes.c_uint64), ("host_chunks", ctypes.c_uint64)]
 
 
 UNIQUE_ID_BYTES = 128  # AT2V_UNIQUE_ID_BYTES (RCCL ncclUniqueId)

@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -30,6 +31,7 @@
 #include "../../include/at2v.h"
 #include "at2v_cache.h"
 #include "at2v_cpu.h"
+#include "at2v_env.h"
 #include "at2v_shard.h"
 
 namespace at2v {
@@ -48,6 +50,7 @@ hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs);
 size_t scratch_bytes_per_block();
 size_t scratch_bytes(int grid);
 int block_threads();
+unsigned kernel_experiments();
 }  // namespace at2v
 
 namespace {
@@ -79,8 +82,7 @@ struct DevBuf {
 // the host learns it from that copy and enqueues a compaction on the build stream (cache_before_launch); no launch waits
 // for it.
 constexpr int kClaimSlots = 8;
-struct PendingBuild {  // a launch's builds not enqueued yet (launch_shard with defer_build: after the caller's copies)
-  bool pending = false;
+struct PendingBuild {  // a launch's builds, enqueued on the build stream after it
   at2v::CacheArgs args{};
   uint32_t max_claims = 0;
   int slot = 0;
@@ -89,12 +91,13 @@ struct SenderCache {
   at2v::CacheArgs args{};
   DevBuf tags[2], entries[2];  // the live tag table / entries ([cur]) and the compaction target ([cur ^ 1])
   int cur = 0;
-  DevBuf payload, free_slots, used, ctl, bcomb, bcomb_lat, seen, claim_list[kClaimSlots];
+  DevBuf payload, free_slots, used, ctl, seen, claim_list[kClaimSlots];
+  const int4* bcomb = nullptr;      // the combs of B, shared by the process's comb contexts on this device (bcomb_acquire)
+  const int4* bcomb_lat = nullptr;
   // Builds run on the context's own stream (the shard's), which a caller's launches on its own streams never use: a
   // separate build stream would share one of the process's 4 hardware queues (GPU_MAX_HW_QUEUES, round robin) with a
   // caller's stream, whose next copy or launch then waited behind a 0.8 ms comb build (config 5 p99).
   hipStream_t build = nullptr;
-  PendingBuild deferred;
   hipEvent_t claims_ready[kClaimSlots] = {};  // launch stream, after the launch that filled slot b
   hipEvent_t slot_free[kClaimSlots] = {};     // build stream, after slot b's flip
   hipEvent_t built = nullptr;                 // build stream, after the last flip
@@ -114,6 +117,38 @@ struct SenderCache {
 // scratch sets per device (AT2V_SCRATCH_SETS overrides, 1..4; 1 = every launch waits for the previous one)
 constexpr int kScratchSets = 2;
 
+// The host-buffer path (at2v_verify_batch, at2v_verify_batch_sharded; round 6, VERDICT r5 "Next" 1). A shard's records go
+// to the device in chunks through kStageSlots pinned staging buffers, so the three stages of consecutive chunks overlap:
+//   host     the copy pool's threads copy chunk i from the caller's (pageable) arrays into slot i % kStageSlots, packed
+//            as pk | sig | rebased offsets | messages;
+//   copy     one DMA upload per chunk on the shard's copy stream, into the slot's device buffer;
+//   compute  the verify launch of chunk i on compute stream i % 2 (two streams: launch i+1 takes the CUs launch i leaves
+//            during its end-of-launch drain), writing the chunk's verdict words of the shard's device bitmap.
+// Slot reuse is ordered by events: the host refills a pinned buffer once its upload is done (`uploaded`, host wait), the
+// copy stream overwrites a device buffer once the launch that read it is done (`consumed`, device wait). The first chunk
+// is small (it is the pipeline's fill: nothing runs on the device until it is up), later ones double up to
+// kStageMaxRecords. Round 1 measured the previous form of this call (pageable hipMemcpyAsync, then verify, then D2H) at
+// 54 M/s against a 78 M/s kernel; the stages were serial.
+constexpr int kStageSlots = 3;
+constexpr size_t kStageMaxRecords = 131072;  // 2,048 wave chunks: one per resident wave of the persistent grid
+constexpr size_t kStageFirstRecords = 32768;
+constexpr size_t kCopyPiece = 1 << 20;       // bytes per copy-pool job item
+constexpr size_t kCopyPoolMin = 2 << 20;     // chunks below this many bytes are copied by the calling thread alone
+struct StageSlot {
+  uint8_t* host = nullptr;  // pinned
+  size_t host_cap = 0;
+  DevBuf dev;
+  hipEvent_t uploaded = nullptr;  // copy stream, after the slot's last upload: the host may refill `host`
+  hipEvent_t consumed = nullptr;  // compute stream, after the last launch that read `dev`: the copy stream may refill it
+};
+struct HostPipe {
+  hipStream_t copy = nullptr;                 // uploads, the verdict download, (sharded) the all-gathers
+  hipStream_t comp[2] = {nullptr, nullptr};   // verify launches of the chunks, alternating
+  hipEvent_t comp_done[2] = {nullptr, nullptr};
+  StageSlot slot[kStageSlots];
+  uint64_t chunks = 0;  // chunks issued by this shard (slot chunks % kStageSlots, compute stream chunks % 2)
+};
+
 struct Shard {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -129,6 +164,7 @@ struct Shard {
   DevBuf btab, pk, sig, msg, off, verdict;
   hipEvent_t copied = nullptr;  // at2v_verify_batch: the verdict copy (the call waits for this, not for the builds)
   SenderCache* cache = nullptr;
+  HostPipe* pipe = nullptr;     // the host-buffer path's streams and staging (created by the first host-buffer call)
 };
 
 }  // namespace
@@ -142,7 +178,14 @@ struct at2v_ctx {
   uint32_t flags = 0;         // at2v_opts.flags (AT2V_CTX_*)
   std::vector<Shard> shards;  // empty: a CPU-backend context (at2v_opts.num_gpus = 0)
   at2v::CpuPool* cpu = nullptr;  // the CPU backend (a CPU context, or AT2V_CTX_CPU_FALLBACK)
-  uint64_t cpu_batches = 0, cpu_fallbacks = 0;
+  at2v::CpuPool* copier = nullptr;  // the host-buffer path's staging copies (created by the first host-buffer call)
+  // atomic: an ingest queue with AT2V_QUEUE_CPU_FALLBACK may fall back from its launcher and its completer thread at once
+  // (both call at2v_verify_batch on the queue's CPU context; the pool serialises the work itself)
+  std::atomic<uint64_t> cpu_batches{0}, cpu_fallbacks{0};
+  // the host-buffer path's chunk schedule (HostPipe; test hooks AT2V_TEST_STAGE_FIRST / _MAX / AT2V_TEST_COPY_THREADS)
+  size_t stage_first = kStageFirstRecords, stage_max = kStageMaxRecords;
+  unsigned copy_threads = 8;
+  uint64_t host_chunks = 0;  // chunks staged by host-buffer calls (at2v_info.host_chunks)
   uint32_t test_fail_launches = 0;  // AT2V_TEST_FAIL_LAUNCH (tests only): that many launches fail before the kernel
   bool partition = true;  // cached launches above pair_max classify, then verify hits and misses apart (AT2V_CACHE_PARTITION)
   ncclComm_t comm = nullptr;  // at2v_comm_init_rank (one rank per process, the context's first device)
@@ -182,7 +225,7 @@ int init_shard(Shard& s, int device) {
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   AT2V_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
-  if (const char* v = std::getenv("AT2V_SCRATCH_SETS")) s.sets = std::min(4, std::max(1, std::atoi(v)));
+  if (const char* v = at2v::test_env("AT2V_SCRATCH_SETS")) s.sets = std::min(4, std::max(1, std::atoi(v)));
   for (int j = 0; j < s.sets; ++j) {
     AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free[j], hipEventDisableTiming));
     AT2V_TRY(hipEventRecord(s.scratch_free[j], s.stream));
@@ -197,12 +240,72 @@ int init_shard(Shard& s, int device) {
 
 bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
+// The combs of B, shared by every comb context of the process on a device (round 6, VERDICT r5 "Next" 3): built by the
+// first context that needs one (on its stream, synchronously, under the registry's lock: a few ms since they are built by
+// additions), freed with the last. A node's ingest queue and its batch contexts hold one 872 MB + 67 MB pair per device
+// instead of one each.
+struct SharedBComb {
+  int device, bits;
+  int4* p;
+  int refs;
+};
+std::mutex g_bcomb_mu;
+std::vector<SharedBComb>& bcomb_registry() {
+  static std::vector<SharedBComb> r;
+  return r;
+}
+
+hipError_t bcomb_acquire(int device, int bits, hipStream_t st, const int4** out) {
+  std::lock_guard<std::mutex> lk(g_bcomb_mu);
+  for (SharedBComb& b : bcomb_registry())
+    if (b.device == device && b.bits == bits) {
+      ++b.refs;
+      *out = b.p;
+      return hipSuccess;
+    }
+  int4* p = nullptr;
+  void* scratch = nullptr;
+  hipError_t e = hipMalloc((void**)&p, at2v::bcomb_bytes(bits));
+  if (e == hipSuccess) e = hipMalloc(&scratch, at2v::bcomb_scratch_bytes());
+#if AT2V_EXP_BCOMB_NOBUILD  // EXPERIMENT (wrong verdicts on the hit path): the hit-list table allocated but never written
+  const bool build = bits == at2v::bcomb_lat_bits();
+#else
+  const bool build = true;
+#endif
+  if (e == hipSuccess && build) e = at2v::launch_build_bcomb(p, bits, scratch, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (scratch) (void)hipFree(scratch);
+  if (e != hipSuccess) {
+    if (p) (void)hipFree(p);
+    return e;
+  }
+  bcomb_registry().push_back({device, bits, p, 1});
+  *out = p;
+  return hipSuccess;
+}
+
+void bcomb_release(const int4* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_bcomb_mu);
+  std::vector<SharedBComb>& r = bcomb_registry();
+  for (size_t i = 0; i < r.size(); ++i)
+    if (r[i].p == p) {
+      if (--r[i].refs == 0) {
+        (void)hipFree(r[i].p);
+        r.erase(r.begin() + (long)i);
+      }
+      return;
+    }
+}
+
 void free_cache(SenderCache*& c) {
   if (!c) return;
   if (c->build) (void)hipStreamSynchronize(c->build);  // (the shard's stream: destroyed with the shard)
   for (DevBuf* b : {&c->tags[0], &c->tags[1], &c->entries[0], &c->entries[1], &c->payload, &c->free_slots, &c->used,
-                    &c->ctl, &c->bcomb, &c->bcomb_lat, &c->seen})
+                    &c->ctl, &c->seen})
     b->release();
+  bcomb_release(c->bcomb);
+  bcomb_release(c->bcomb_lat);
   for (DevBuf& b : c->claim_list) b.release();
   if (c->built) (void)hipEventDestroy(c->built);
   if (c->compacted) (void)hipEventDestroy(c->compacted);
@@ -235,7 +338,7 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit
   a.admit_first = admit_first ? 1 : 0;
   // the sighting filter: 2^21 fingerprints (16 MB), so a key seen twice within ~a million records is still found
   a.seen_mask = (1u << 21) - 1;
-  if (const char* b = std::getenv("AT2V_TEST_CACHE_FP_BITS")) {
+  if (const char* b = at2v::test_env("AT2V_TEST_CACHE_FP_BITS")) {
     const int bits = std::atoi(b);
     if (bits > 0 && bits < 64) a.fp_mask = (1ull << bits) - 1ull;
   }
@@ -267,14 +370,10 @@ int init_cache(Shard& s, uint32_t capacity, uint64_t seed, bool comb, bool admit
                // ones for the hit-list kernel, 24-bit with AT2V_CTX_BCOMB_WIDE
     const int lat_bits = at2v::bcomb_lat_bits();
     const int bits = bcomb_wide ? at2v::bcomb_wide_bits() : at2v::bcomb_mid_bits();
-    AT2V_TRY(c->bcomb_lat.ensure(at2v::bcomb_bytes(lat_bits)));
-    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb_lat.p, lat_bits, s.stream));
-    AT2V_TRY(c->bcomb.ensure(at2v::bcomb_bytes(bits)));
-#if !AT2V_EXP_BCOMB_NOBUILD  // EXPERIMENT (wrong verdicts on the hit path): the table allocated but never written
-    AT2V_TRY(at2v::launch_build_bcomb((int4*)c->bcomb.p, bits, s.stream));
-#endif
-    a.bcomb_lat = (const int4*)c->bcomb_lat.p;
-    a.bcomb = (const int4*)c->bcomb.p;
+    AT2V_TRY(bcomb_acquire(s.device, lat_bits, s.stream, &c->bcomb_lat));
+    AT2V_TRY(bcomb_acquire(s.device, bits, s.stream, &c->bcomb));
+    a.bcomb_lat = c->bcomb_lat;
+    a.bcomb = c->bcomb;
     a.bcomb_bits = bits;
   }
   AT2V_TRY(at2v::launch_cache_init(a, s.stream));
@@ -358,14 +457,6 @@ hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
   return e;
 }
 
-// after launch_shard(.., defer_build = true) and the caller's own work on the shard stream (its verdict copy, the
-// all-gather): the deferred builds
-hipError_t flush_cache_build(Shard& s) {
-  if (!s.cache || !s.cache->deferred.pending) return hipSuccess;
-  s.cache->deferred.pending = false;
-  return enqueue_cache_build(*s.cache, s.cache->deferred);
-}
-
 // One verify launch on shard s (current device = s.device), on `stream`. The launch takes the shard's next scratch set
 // and waits for the launch that last used that set, on whatever stream that ran; launches on different streams may
 // therefore run concurrently (on one stream they are ordered anyway). Cached launches may overlap too: they share the tag
@@ -373,7 +464,7 @@ hipError_t flush_cache_build(Shard& s) {
 // after a compaction waits for it (cache_before_launch). The verdict words are zeroed first (fail closed).
 hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                         uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream,
-                        bool zero_verdicts = true, bool defer_build = false) {
+                        bool zero_verdicts = true) {
   if (ctx->test_fail_launches) {  // test hook: a launch failure, as a faulting device would report it
     --ctx->test_fail_launches;
     return hipErrorLaunchFailure;
@@ -413,17 +504,190 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   if (e == hipSuccess && c) {
     // claims of this launch -> payloads on the build stream (later launches use them; this one did not wait)
     e = hipEventRecord(c->claims_ready[cs], stream);
-    PendingBuild b{true, ca, std::min(n, ca.capacity), cs};
-    if (e == hipSuccess) {
-      if (defer_build) c->deferred = b;  // the caller enqueues it after its own work on the shard stream
-      else e = enqueue_cache_build(*c, b);
-    }
+    if (e == hipSuccess) e = enqueue_cache_build(*c, PendingBuild{ca, std::min(n, ca.capacity), cs});
   }
   if (e == hipSuccess) e = hipEventRecord(s.scratch_free[j], stream);
   return e;
 }
 
+// ---- the host-buffer path: chunked, pipelined staging (HostPipe above) ----
+
+void free_pipe(Shard& s) {
+  HostPipe* p = s.pipe;
+  if (!p) return;
+  for (hipStream_t st : {p->copy, p->comp[0], p->comp[1]})
+    if (st) (void)hipStreamSynchronize(st);
+  for (StageSlot& sl : p->slot) {
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.dev.release();
+    for (hipEvent_t ev : {sl.uploaded, sl.consumed})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  for (hipEvent_t ev : p->comp_done)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipStream_t st : {p->copy, p->comp[0], p->comp[1]})
+    if (st) (void)hipStreamDestroy(st);
+  delete p;
+  s.pipe = nullptr;
+}
+
+// the shard's pipe (current device = s.device); its events are recorded once, so the first waits are no-ops
+hipError_t ensure_pipe(Shard& s) {
+  if (s.pipe) return hipSuccess;
+  HostPipe* p = new (std::nothrow) HostPipe;
+  if (!p) return hipErrorOutOfMemory;
+  s.pipe = p;
+  hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
+  for (int j = 0; j < 2 && e == hipSuccess; ++j) {
+    e = hipStreamCreateWithFlags(&p->comp[j], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->comp_done[j], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(p->comp_done[j], p->copy);
+  }
+  for (StageSlot& sl : p->slot) {
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(sl.uploaded, p->copy);
+    if (e == hipSuccess) e = hipEventRecord(sl.consumed, p->copy);
+  }
+  if (e != hipSuccess) free_pipe(s);
+  return e;
+}
+
+// A staged chunk of c records with mb message bytes: pk | sig | offsets (c + 1, rebased) | messages (+16 bytes of slack
+// for the kernels' last-word reads), every part 16-byte aligned.
+struct ChunkLayout {
+  size_t sig, off, msg, upload, total;
+};
+ChunkLayout chunk_layout(size_t c, size_t mb) {
+  ChunkLayout l;
+  l.sig = c * 32;
+  l.off = c * 96;
+  l.msg = (l.off + (c + 1) * 4 + 15) & ~(size_t)15;
+  l.upload = l.msg + mb;
+  l.total = l.upload + 16;
+  return l;
+}
+
+// The host copy of one chunk, split into pieces of about kCopyPiece bytes for the copy pool.
+struct CopyPiece {
+  uint8_t* dst;
+  const uint8_t* src;  // bytes, or (offsets piece) the caller's msg_off + first record
+  size_t len;          // bytes, or offsets
+  uint32_t base;       // offsets piece: subtracted from every offset
+  bool offsets;
+};
+struct CopyJob {
+  std::vector<CopyPiece> pieces;
+  void add(uint8_t* dst, const uint8_t* src, size_t len) {
+    for (size_t o = 0; o < len; o += kCopyPiece)
+      pieces.push_back({dst + o, src + o, std::min(kCopyPiece, len - o), 0, false});
+  }
+  void add_offsets(uint32_t* dst, const uint32_t* src, size_t count, uint32_t base) {
+    const size_t step = kCopyPiece / 4;
+    for (size_t o = 0; o < count; o += step)
+      pieces.push_back({(uint8_t*)(dst + o), (const uint8_t*)(src + o), std::min(step, count - o), base, true});
+  }
+  static void run_piece(void* a, size_t i) {
+    const CopyPiece& p = static_cast<CopyJob*>(a)->pieces[i];
+    if (!p.offsets) {
+      std::memcpy(p.dst, p.src, p.len);
+      return;
+    }
+    const uint32_t* s = (const uint32_t*)p.src;
+    uint32_t* d = (uint32_t*)p.dst;
+    for (size_t k = 0; k < p.len; ++k) d[k] = s[k] - p.base;
+  }
+};
+
+// Records [a, a + c) of the caller's batch (absolute indices; a multiple of 64 relative to the shard's first record, so
+// the chunk owns whole verdict words) -> staging slot -> device -> verify launch writing d_words (the chunk's words of
+// the shard's device bitmap, zeroed by the launch first). Current device = s.device. Returns after the launch is
+// enqueued; the host waits only for the slot's previous upload (and, when the slot must grow, for its previous launch).
+hipError_t issue_chunk(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, const uint8_t* pk, const uint8_t* sig,
+                       const uint8_t* msg, const uint32_t* msg_off, size_t a, size_t c, uint32_t* d_words) {
+  HostPipe& p = *s.pipe;
+  StageSlot& sl = p.slot[p.chunks % kStageSlots];
+  const int j = (int)(p.chunks % 2);
+  const uint32_t mb0 = msg_off[a];
+  const size_t mb = (size_t)(msg_off[a + c] - mb0);
+  const ChunkLayout L = chunk_layout(c, mb);
+  hipError_t e = hipEventSynchronize(sl.uploaded);
+  if (e == hipSuccess && (sl.host_cap < L.total || sl.dev.cap < L.total)) {
+    e = hipEventSynchronize(sl.consumed);  // (the slot's device buffer is freed by a regrow)
+    if (e == hipSuccess && sl.host_cap < L.total) {
+      if (sl.host) (void)hipHostFree(sl.host);
+      sl.host = nullptr;
+      sl.host_cap = 0;
+      const size_t want = std::max(L.total + L.total / 4, chunk_layout(ctx->stage_max, 0).total);
+      e = hipHostMalloc((void**)&sl.host, want, hipHostMallocDefault);
+      if (e == hipSuccess) sl.host_cap = want;
+    }
+    if (e == hipSuccess) e = sl.dev.ensure(std::max(L.total, sl.host_cap));
+  }
+  if (e != hipSuccess) return e;
+  CopyJob job;
+  job.add(sl.host, pk + a * 32, c * 32);
+  job.add(sl.host + L.sig, sig + a * 64, c * 64);
+  job.add_offsets((uint32_t*)(sl.host + L.off), msg_off + a, c + 1, mb0);
+  if (mb) job.add(sl.host + L.msg, msg + mb0, mb);
+  if (copier && L.upload >= kCopyPoolMin) {
+    at2v::pool_run(copier, job.pieces.size(), CopyJob::run_piece, &job);
+  } else {
+    for (size_t i = 0; i < job.pieces.size(); ++i) CopyJob::run_piece(&job, i);
+  }
+  uint8_t* d = (uint8_t*)sl.dev.p;
+  e = hipStreamWaitEvent(p.copy, sl.consumed, 0);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, sl.host, L.upload, hipMemcpyHostToDevice, p.copy);
+  if (e == hipSuccess) e = hipEventRecord(sl.uploaded, p.copy);
+  if (e == hipSuccess) e = hipStreamWaitEvent(p.comp[j], sl.uploaded, 0);
+  if (e == hipSuccess)
+    e = launch_shard(ctx, s, d, d + L.sig, d + L.msg, (uint32_t)mb, (const uint32_t*)(d + L.off), (uint32_t)c, d_words,
+                     p.comp[j]);
+  if (e == hipSuccess) e = hipEventRecord(sl.consumed, p.comp[j]);
+  if (e == hipSuccess) e = hipEventRecord(p.comp_done[j], p.comp[j]);
+  ++p.chunks;
+  ++ctx->host_chunks;
+  return e;
+}
+
+// The chunk schedule of one shard's part of a host batch: kStageFirstRecords (or, if larger, one wave chunk more than
+// the low-latency kernel takes), doubling up to kStageMaxRecords; a remainder smaller than the first chunk joins the
+// chunk before it. Every chunk but the last is a multiple of 64 records.
+struct ChunkPlan {
+  size_t first = 0, next = 0, pos = 0, m = 0, cap = 0;
+  void init(size_t m_, const at2v_ctx* ctx) {
+    m = m_;
+    pos = 0;
+    first = std::max(ctx->stage_first, ((size_t)ctx->pair_max + 64) / 64 * 64);
+    cap = std::max(ctx->stage_max, first);
+    next = first;
+  }
+  bool done() const { return pos >= m; }
+  size_t take() {  // the next chunk's record count (its first record is pos before the call)
+    size_t c = std::min(next, m - pos);
+    if (m - pos - c < first) c = m - pos;
+    next = std::min(next * 2, cap);
+    pos += c;
+    return c;
+  }
+};
+
+at2v::CpuPool* copy_pool(at2v_ctx* ctx) {
+  if (!ctx->copier && ctx->copy_threads > 1)
+    ctx->copier = at2v::copy_pool_create(std::min(ctx->copy_threads, at2v::usable_cpus()));
+  return ctx->copier;  // (nullptr: the calling thread copies alone)
+}
+
 int nccl_code(ncclResult_t r) { return r == ncclSuccess ? AT2V_OK : AT2V_E_RCCL; }
+
+// AT2V_EXPERIMENT_* bits of this library: the kernels object's switches and this file's
+unsigned library_experiments() {
+  unsigned m = at2v::kernel_experiments();
+#if AT2V_EXP_BCOMB_NOBUILD
+  m |= AT2V_EXPERIMENT_BCOMB_NOBUILD;
+#endif
+  return m;
+}
 
 // The collective step of a rank (current device = its shard's): zero this rank's slice `mine` of the node bitmap,
 // verify its records into it unless an earlier local step already failed (`local` != AT2V_OK), then ALWAYS join the
@@ -473,6 +737,11 @@ extern "C" {
 int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   if (!out) return AT2V_E_INVALID;
   *out = nullptr;
+  // a timing-experiment build (wrong verdicts) serves no context unless the process explicitly allows it
+  if (library_experiments()) {
+    const char* allow = std::getenv("AT2V_ALLOW_EXPERIMENT");
+    if (!allow || std::strcmp(allow, "1") != 0) return AT2V_E_INVALID;
+  }
   at2v_opts o{0, 1, AT2V_POLICY_DALEK_V1, 0, 0, 0, 0, 0};
   if (opts) o = *opts;
   if (o.num_gpus < 0 || o.num_gpus > 64) return AT2V_E_INVALID;
@@ -493,7 +762,7 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   }
   // AT2V_TEST_DEVICE_ALIAS (tests only): shard g runs on device (device + g) % ndev, so a one-GPU box executes the
   // single-process multi-device path (split, per-shard streams, scratch, B tables and caches) with num_gpus > ndev
-  const bool alias = std::getenv("AT2V_TEST_DEVICE_ALIAS") && std::atoi(std::getenv("AT2V_TEST_DEVICE_ALIAS")) != 0;
+  const bool alias = at2v::test_env_long("AT2V_TEST_DEVICE_ALIAS", 0) != 0;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return AT2V_E_NODEVICE;
   if (o.device < 0 || o.device >= ndev || (!alias && o.device + o.num_gpus > ndev)) return AT2V_E_NODEVICE;
@@ -501,8 +770,13 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   if (!c) return AT2V_E_OOM;
   c->policy = o.policy;
   c->flags = o.flags;
-  if (const char* v = std::getenv("AT2V_TEST_FAIL_LAUNCH")) c->test_fail_launches = (uint32_t)std::strtoul(v, nullptr, 10);
-  if (const char* v = std::getenv("AT2V_CACHE_PARTITION")) c->partition = std::atoi(v) != 0;  // (A/B: 0 = round 4)
+  c->test_fail_launches = (uint32_t)at2v::test_env_long("AT2V_TEST_FAIL_LAUNCH", 0);
+  c->partition = at2v::test_env_long("AT2V_CACHE_PARTITION", 1) != 0;  // (A/B: 0 = round 4)
+  c->stage_first = (size_t)at2v::test_env_long("AT2V_TEST_STAGE_FIRST", (long)kStageFirstRecords) / 64 * 64;
+  c->stage_max = (size_t)at2v::test_env_long("AT2V_TEST_STAGE_MAX", (long)kStageMaxRecords) / 64 * 64;
+  c->copy_threads = (unsigned)at2v::test_env_long("AT2V_TEST_COPY_THREADS", 8);
+  if (c->stage_first < 64) c->stage_first = 64;
+  if (c->stage_max < c->stage_first) c->stage_max = c->stage_first;
   c->pair_max = o.small_batch_max == 0 ? AT2V_SMALL_BATCH_DEFAULT
                 : o.small_batch_max == AT2V_SMALL_BATCH_OFF ? 0u : o.small_batch_max;
   c->shards.resize((size_t)o.num_gpus);
@@ -510,8 +784,7 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   (void)hipGetDevice(&prev);
   std::random_device rd;
   // test hook (A/B runs of processes the caller does not configure, e.g. the config-5 mini-network's nodes)
-  const char* wide_v = std::getenv("AT2V_BCOMB_WIDE");
-  const bool wide_env = wide_v && std::atoi(wide_v) != 0;
+  const bool wide_env = at2v::test_env_long("AT2V_BCOMB_WIDE", 0) != 0;
   for (int g = 0; g < o.num_gpus; ++g) {
     int rc = init_shard(c->shards[(size_t)g], alias ? (o.device + g) % ndev : o.device + g);
     if (rc == AT2V_OK && o.sender_cache)
@@ -542,6 +815,8 @@ void at2v_destroy(at2v_ctx* ctx) {
   for (Shard& s : ctx->shards) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.pipe)
+      for (hipStream_t st : {s.pipe->copy, s.pipe->comp[0], s.pipe->comp[1]}) (void)hipStreamSynchronize(st);
     for (hipEvent_t ev : s.scratch_free)
       if (ev) (void)hipEventSynchronize(ev);
   }
@@ -562,6 +837,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     for (hipEvent_t ev : s.scratch_free)
       if (ev) (void)hipEventDestroy(ev);
     if (s.copied) (void)hipEventDestroy(s.copied);
+    free_pipe(s);
     free_cache(s.cache);
     for (DevBuf& b : s.scratch) b.release();
     for (DevBuf& b : s.part) b.release();
@@ -574,6 +850,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   at2v::cpu_pool_destroy(ctx->cpu);
+  at2v::cpu_pool_destroy(ctx->copier);
   delete ctx;
 }
 
@@ -593,51 +870,68 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
   (void)hipGetDevice(&prev);
   const size_t G = ctx->shards.size();
   int rc = AT2V_OK;
-  std::vector<std::vector<uint32_t>> offs_all(G);  // must outlive the async uploads
-  for (size_t g = 0; g < G && rc == AT2V_OK; ++g) {
-    Shard& s = ctx->shards[g];
-    const at2v::Range r = at2v::device_range(n, G, g);  // 64-aligned: the shard's words start at word lo/32
-    const size_t a = r.lo, m = r.size();
-    if (m == 0) continue;
-    hipError_t e = hipSetDevice(s.device);
-    const uint32_t mb0 = msg_off[a];
-    const size_t mbytes = (size_t)(msg_off[a + m] - mb0);
-    if (e == hipSuccess) e = s.pk.ensure(m * 32);
-    if (e == hipSuccess) e = s.sig.ensure(m * 64);
-    if (e == hipSuccess) e = s.msg.ensure(mbytes + 16);
-    if (e == hipSuccess) e = s.off.ensure((m + 1) * 4);
-    if (e == hipSuccess) e = s.verdict.ensure(((m + 31) / 32) * 4);
-    std::vector<uint32_t>& offs = offs_all[g];  // offsets rebased to the shard's message slice
-    offs.resize(m + 1);
-    at2v::rebase_offsets(msg_off, a, m, offs.data());
-    if (e == hipSuccess) e = hipMemcpyAsync(s.pk.p, pk + a * 32, m * 32, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.sig.p, sig + a * 64, m * 64, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess && mbytes)
-      e = hipMemcpyAsync(s.msg.p, msg + mb0, mbytes, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.off.p, offs.data(), (m + 1) * 4, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess)
-      e = launch_shard(ctx, s, (const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
-                       (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (uint32_t*)s.verdict.p, s.stream,
-                       true, /*defer_build=*/true);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(verdicts + a / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, s.stream);
-    if (e == hipSuccess) e = hipEventRecord(s.copied, s.stream);
-    const hipError_t eb = flush_cache_build(s);  // (the next call's uploads follow the builds on this stream)
-    if (e == hipSuccess) e = eb;
-    if (e != hipSuccess) rc = hip_code(e);
-  }
-  // shards run concurrently on their own devices/streams; wait for all of them (not for the builds behind them)
+  at2v::CpuPool* copier = copy_pool(ctx);
+  // Per shard (64-aligned index range: its words start at word lo/32 of the caller's array): the device bitmap and the
+  // pipe, then the chunks of all shards round robin, so every device's pipeline fills early and the copy pool serves
+  // them in turn.
+  std::vector<ChunkPlan> plan(G);
+  std::vector<size_t> lo(G);
+  std::vector<hipError_t> err(G, hipSuccess);
   for (size_t g = 0; g < G; ++g) {
     Shard& s = ctx->shards[g];
-    if (hipSetDevice(s.device) != hipSuccess) continue;
+    const at2v::Range r = at2v::device_range(n, G, g);
+    lo[g] = r.lo;
+    plan[g].init(r.size(), ctx);
+    if (r.size() == 0) continue;
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = s.verdict.ensure(((r.size() + 31) / 32) * 4);
+    if (e == hipSuccess) e = ensure_pipe(s);
+    err[g] = e;
+  }
+  for (bool more = true; more;) {
+    more = false;
+    for (size_t g = 0; g < G; ++g) {
+      ChunkPlan& cp = plan[g];
+      if (cp.done() || err[g] != hipSuccess) continue;
+      Shard& s = ctx->shards[g];
+      const size_t at = cp.pos, c = cp.take();
+      err[g] = hipSetDevice(s.device);
+      if (err[g] == hipSuccess)
+        err[g] = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, lo[g] + at, c, (uint32_t*)s.verdict.p + at / 32);
+      more = more || !cp.done();
+    }
+  }
+  // the verdict words of each shard, once its last two launches are done (copy stream)
+  for (size_t g = 0; g < G; ++g) {
+    Shard& s = ctx->shards[g];
+    const size_t m = plan[g].m;
+    if (m == 0) continue;
+    hipError_t e = err[g];
+    if (e == hipSuccess) e = hipSetDevice(s.device);
+    HostPipe* p = s.pipe;
+    for (int j = 0; j < 2 && e == hipSuccess; ++j) e = hipStreamWaitEvent(p->copy, p->comp_done[j], 0);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(verdicts + lo[g] / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, p->copy);
+    if (e == hipSuccess) e = hipEventRecord(s.copied, p->copy);
+    err[g] = e;
+    if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
+  }
+  // shards run concurrently on their own devices/streams; wait for all of them (not for the cache builds behind them)
+  for (size_t g = 0; g < G; ++g) {
+    Shard& s = ctx->shards[g];
+    if (plan[g].m == 0 || err[g] != hipSuccess || hipSetDevice(s.device) != hipSuccess) continue;
     hipError_t e = hipEventSynchronize(s.copied);
     if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
   if (rc != AT2V_OK && ctx->cpu) {
     // AT2V_CTX_CPU_FALLBACK: the records are still in the caller's host buffers. Drain what the shards enqueued (no
     // verdict copy of this call may land after the CPU's words), then verify the whole batch on the CPU backend.
-    for (Shard& s : ctx->shards)
-      if (hipSetDevice(s.device) == hipSuccess) (void)hipStreamSynchronize(s.stream);
+    for (Shard& s : ctx->shards) {
+      if (hipSetDevice(s.device) != hipSuccess) continue;
+      (void)hipStreamSynchronize(s.stream);
+      if (s.pipe)
+        for (hipStream_t st : {s.pipe->copy, s.pipe->comp[0], s.pipe->comp[1]}) (void)hipStreamSynchronize(st);
+    }
     at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
     ++ctx->cpu_batches;
     ++ctx->cpu_fallbacks;
@@ -698,7 +992,7 @@ int at2v_comm_init_rank(at2v_ctx* ctx, const uint8_t unique_id[AT2V_UNIQUE_ID_BY
     rc = hip_code(hipEventCreateWithFlags(&ctx->gather_done, hipEventDisableTiming));
     if (rc == AT2V_OK) rc = hip_code(hipEventRecord(ctx->gather_done, ctx->shards[0].stream));  // first wait: no-op
   }
-  if (rc == AT2V_OK && std::getenv("AT2V_TEST_FAIL_COMM_SETUP")) rc = AT2V_E_HIP;  // test hook: a local set-up failure
+  if (rc == AT2V_OK && at2v::test_env("AT2V_TEST_FAIL_COMM_SETUP")) rc = AT2V_E_HIP;  // test hook: a local set-up failure
   // collective: blocks until all `world` ranks have called it (a rank that failed above still joins, then reports)
   const int rn = nccl_code(ncclCommInitRank(&ctx->comm, world, id, rank));
   if (rn == AT2V_OK) {  // every rank that holds a communicator joins the outcome all-reduce, whatever failed locally
@@ -764,37 +1058,36 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
   int prev = 0;
   (void)hipGetDevice(&prev);
   hipError_t e = hipSetDevice(s.device);
-  std::vector<uint32_t> offs(m + 1, 0u);
-  if (m) at2v::rebase_offsets(msg_off, a, m, offs.data());
-  const uint32_t mb0 = m ? msg_off[a] : 0;
-  const size_t mbytes = offs[m];
-  // Local steps (staging, upload, verify into this rank's wpr words). A failure here is this rank's alone: it still
-  // joins every collective below, sending zero words (fail closed), and every rank learns of it.
+  // Local steps: this rank's range through the chunked pipeline (HostPipe) into its wpr words, pad words zeroed. A failure
+  // here is this rank's alone: it still joins every collective below, sending zero words (fail closed), and every rank
+  // learns of it. The collectives run on the pipe's copy stream (the context's own stream if the pipe could not be made),
+  // behind the chunks' launches; the sender cache's builds run on the context's stream and do not delay them.
   if (e == hipSuccess) e = s.verdict.ensure(wpr * 4);
+  if (e == hipSuccess) e = ensure_pipe(s);
+  hipStream_t st = s.pipe ? s.pipe->copy : s.stream;
+  const size_t used = (m + 31) / 32;  // words the chunks' launches write (each zeroes its own first)
+  if (e == hipSuccess && used < wpr)
+    e = hipMemsetAsync((uint32_t*)s.verdict.p + used, 0, (wpr - used) * 4, st);  // pad words (an empty rank: all)
   if (e == hipSuccess && m) {
-    e = s.pk.ensure(m * 32);
-    if (e == hipSuccess) e = s.sig.ensure(m * 64);
-    if (e == hipSuccess) e = s.msg.ensure(mbytes + 16);
-    if (e == hipSuccess) e = s.off.ensure((m + 1) * 4);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.pk.p, pk + a * 32, m * 32, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.sig.p, sig + a * 64, m * 64, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess && mbytes) e = hipMemcpyAsync(s.msg.p, msg + mb0, mbytes, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.off.p, offs.data(), (m + 1) * 4, hipMemcpyHostToDevice, s.stream);
+    at2v::CpuPool* copier = copy_pool(ctx);
+    ChunkPlan cp;
+    cp.init(m, ctx);
+    while (e == hipSuccess && !cp.done()) {
+      const size_t at = cp.pos, c = cp.take();
+      e = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, a + at, c, (uint32_t*)s.verdict.p + at / 32);
+    }
+    for (int j = 0; j < 2 && e == hipSuccess; ++j) e = hipStreamWaitEvent(st, s.pipe->comp_done[j], 0);
   }
-  if (e == hipSuccess) e = hipMemsetAsync(s.verdict.p, 0, wpr * 4, s.stream);  // pad words are 0
-  if (e == hipSuccess && m)
-    e = launch_shard(ctx, s, (const uint8_t*)s.pk.p, (const uint8_t*)s.sig.p, (const uint8_t*)s.msg.p,
-                     (uint32_t)mbytes, (const uint32_t*)s.off.p, (uint32_t)m, (uint32_t*)s.verdict.p, s.stream,
-                     /*zero_verdicts=*/false, /*defer_build=*/true);
   int rc = hip_code(e);
   // The all-gather runs in rounds of at most kGatherWindow words per rank through buffers allocated at
   // at2v_comm_init_rank, so no allocation stands between a rank and the collectives: every rank issues the same
   // ceil(wpr / window) all-gathers whatever happened locally.
+  if (ctx->gather_done) (void)hipStreamWaitEvent(st, ctx->gather_done, 0);
   const size_t W = kGatherWindow;
   for (size_t j0 = 0; j0 < wpr; j0 += W) {
     const size_t cnt = std::min(W, wpr - j0);
     const void* send = rc == AT2V_OK ? (const void*)((const uint32_t*)s.verdict.p + j0) : ctx->zeros.p;
-    const ncclResult_t rr = ncclAllGather(send, ctx->window.p, cnt, ncclUint32, ctx->comm, s.stream);
+    const ncclResult_t rr = ncclAllGather(send, ctx->window.p, cnt, ncclUint32, ctx->comm, st);
     ++ctx->gathers;
     if (rr != ncclSuccess && rc == AT2V_OK) rc = AT2V_E_RCCL;
     // rank q's words [j0, j0 + cnt) are at window word q * cnt; its real words go to word lo_q/32 + j0 of verdicts
@@ -803,25 +1096,24 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
       if (wc.words <= j0) continue;
       const size_t k = std::min(cnt, wc.words - j0);
       const hipError_t ec = hipMemcpyAsync(verdicts + wc.dst_word + j0, (const uint32_t*)ctx->window.p + (size_t)q * cnt,
-                                           k * 4, hipMemcpyDeviceToHost, s.stream);
+                                           k * 4, hipMemcpyDeviceToHost, st);
       if (ec != hipSuccess && rc == AT2V_OK) rc = hip_code(ec);
     }
-    const hipError_t es = hipStreamSynchronize(s.stream);  // the window is reused by the next round
+    const hipError_t es = hipStreamSynchronize(st);  // the window is reused by the next round
     if (es != hipSuccess && rc == AT2V_OK) rc = hip_code(es);
   }
-  if (ctx->gather_done) (void)hipEventRecord(ctx->gather_done, s.stream);
+  if (ctx->gather_done) (void)hipEventRecord(ctx->gather_done, st);
   // Every rank learns whether any rank failed: a peer's failure turns this rank's success into AT2V_E_PEER, so no
   // rank hands a bitmap with a zeroed (fail-closed) slice to its apply step as if it were complete.
   int any = rc != AT2V_OK;
-  hipError_t es = hipMemsetD32Async((hipDeviceptr_t)ctx->status.p, any, 1, s.stream);
-  const ncclResult_t ra = ncclAllReduce(ctx->status.p, ctx->status.p, 1, ncclInt32, ncclMax, ctx->comm, s.stream);
+  hipError_t es = hipMemsetD32Async((hipDeviceptr_t)ctx->status.p, any, 1, st);
+  const ncclResult_t ra = ncclAllReduce(ctx->status.p, ctx->status.p, 1, ncclInt32, ncclMax, ctx->comm, st);
   int got = 1;
-  if (es == hipSuccess) es = hipMemcpyAsync(&got, ctx->status.p, 4, hipMemcpyDeviceToHost, s.stream);
-  if (es == hipSuccess) es = hipStreamSynchronize(s.stream);
+  if (es == hipSuccess) es = hipMemcpyAsync(&got, ctx->status.p, 4, hipMemcpyDeviceToHost, st);
+  if (es == hipSuccess) es = hipStreamSynchronize(st);
   if (rc == AT2V_OK && ra != ncclSuccess) rc = AT2V_E_RCCL;
   if (rc == AT2V_OK && es != hipSuccess) rc = hip_code(es);
   if (rc == AT2V_OK && got) rc = AT2V_E_PEER;
-  (void)flush_cache_build(s);  // after the collectives (a failed enqueue only leaves keys unbuilt)
   (void)hipSetDevice(prev);
   return rc;
 }
@@ -951,6 +1243,8 @@ int at2v_get_info(at2v_ctx* ctx, at2v_info* out) {
   out->cpu_threads = at2v::cpu_pool_threads(ctx->cpu);
   out->cpu_batches = ctx->cpu_batches;
   out->cpu_fallbacks = ctx->cpu_fallbacks;
+  out->experiments = library_experiments();
+  out->host_chunks = ctx->host_chunks;
   if (ctx->shards.empty()) return AT2V_OK;  // CPU context: no device geometry
   const Shard& s = ctx->shards[0];
   out->num_gpus = (int)ctx->shards.size();

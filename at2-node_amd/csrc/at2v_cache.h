@@ -82,7 +82,10 @@ size_t bcomb_bytes(int bits);          // a comb of B with bits-bit windows (16,
 int bcomb_lat_bits();
 int bcomb_mid_bits();
 int bcomb_wide_bits();
-hipError_t launch_build_bcomb(int4* out, int bits, hipStream_t stream);
+// build a comb of B into out (bcomb_bytes(bits)), asynchronously on stream; scratch: bcomb_scratch_bytes() of device
+// memory the launches use until they complete
+size_t bcomb_scratch_bytes();
+hipError_t launch_build_bcomb(int4* out, int bits, void* scratch, hipStream_t stream);
 int cache_ctl_words();
 // ctl word indices the host reads (at2v_get_info) and resets
 enum CacheCtlWord : int {

@@ -22,6 +22,11 @@ CpuPool* cpu_pool_create(unsigned threads);
 void cpu_pool_destroy(CpuPool* p);
 unsigned cpu_pool_threads(const CpuPool* p);
 
+// A pool without the verify tables, for host work of the GPU path (the staging copies of at2v_verify_batch), and its
+// generic job: fn(arg, c) for c = 0..chunks-1 over the workers and the caller, synchronous. One job at a time per pool.
+CpuPool* copy_pool_create(unsigned threads);
+void pool_run(CpuPool* p, size_t chunks, void (*fn)(void*, size_t), void* arg);
+
 // n records in the at2v_verify_batch layout -> ceil(n/32) verdict words (pad bits 0), synchronous. Chunks of 64 records
 // own their two words, so workers never share a word. One batch at a time per pool (calls serialise).
 void cpu_verify_batch(CpuPool* p, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint32_t* msg_off,

@@ -14,6 +14,7 @@
 #include <new>
 
 #include "../../include/at2v.h"
+#include "at2v_env.h"
 #include "at2v_ledger.h"
 #include "at2v_pack.h"
 #include "at2v_queue.h"
@@ -102,12 +103,12 @@ struct HipBackend {
       if (rc) return rc;
     }
     device = o.device;
-    if (const char* v = std::getenv("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
-    if (const char* v = std::getenv("AT2V_QUEUE_ZEROCOPY")) zerocopy_max = (uint32_t)std::strtoul(v, nullptr, 10);
-    if (const char* v = std::getenv("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
+    if (const char* v = at2v::test_env("AT2V_QUEUE_DIRECT")) direct = std::atoi(v) != 0;
+    if (const char* v = at2v::test_env("AT2V_QUEUE_ZEROCOPY")) zerocopy_max = (uint32_t)std::strtoul(v, nullptr, 10);
+    if (const char* v = at2v::test_env("AT2V_QUEUE_SPIN_US")) spin_us = (uint32_t)std::strtoul(v, nullptr, 10);
     if (o.flags & AT2V_QUEUE_EAGER) ncomp = 1;
-    if (const char* v = std::getenv("AT2V_QUEUE_STREAMS")) ncomp = std::atoi(v) == 1 ? 1 : 2;
-    if (const char* v = std::getenv("AT2V_QUEUE_PRIORITY")) prio = std::atoi(v) != 0;
+    if (const char* v = at2v::test_env("AT2V_QUEUE_STREAMS")) ncomp = std::atoi(v) == 1 ? 1 : 2;
+    if (const char* v = at2v::test_env("AT2V_QUEUE_PRIORITY")) prio = std::atoi(v) != 0;
     const DeviceScope scope(device);
     if (scope.err != hipSuccess) return AT2V_E_HIP;
     int least = 0, greatest = 0;
@@ -313,7 +314,7 @@ int at2v_queue_create(const at2v_queue_opts* opts, at2v_queue** out) {
   if (o.max_msg_bytes) qo.max_msg_bytes = o.max_msg_bytes;
   if (o.depth) qo.depth = (int)o.depth;
   qo.eager = (o.flags & AT2V_QUEUE_EAGER) != 0;
-  if (const char* v = std::getenv("AT2V_QUEUE_LAUNCH_HERE")) qo.launch_here = std::atoi(v) != 0;  // (A/B)
+  if (const char* v = at2v::test_env("AT2V_QUEUE_LAUNCH_HERE")) qo.launch_here = std::atoi(v) != 0;  // (A/B)
   if (o.flags & ~(AT2V_QUEUE_EAGER | AT2V_QUEUE_SENDER_COMB | AT2V_QUEUE_CPU | AT2V_QUEUE_CPU_FALLBACK))
     return AT2V_E_INVALID;
   if ((o.flags & AT2V_QUEUE_CPU) && (o.flags & (AT2V_QUEUE_SENDER_COMB | AT2V_QUEUE_CPU_FALLBACK))) return AT2V_E_INVALID;

@@ -31,7 +31,7 @@ pub struct At2vLedger {
 
 /// include/at2v.h AT2V_ABI_VERSION: the layouts of the #[repr(C)] structs below. `BatchVerifier::new` and
 /// `Queue::new` refuse a library that reports another version (the structs are copied whole by the library).
-pub const AT2V_ABI_VERSION: c_int = 6;
+pub const AT2V_ABI_VERSION: c_int = 7;
 
 pub const AT2V_POLICY_DALEK_V1: c_int = 0;
 pub const AT2V_POLICY_LIBSODIUM_1_0_18: c_int = 1;
@@ -102,6 +102,14 @@ pub const AT2V_CTX_ADMIT_FIRST: u32 = 2;
 /// `At2vOpts::flags`: with sender_comb, the throughput kernel's comb of B with 24-bit windows (11.8 GB, default 20-bit).
 pub const AT2V_CTX_BCOMB_WIDE: u32 = 4;
 
+/// `At2vInfo::experiments` bits: timing-only builds with wrong verdicts (at2v_create refuses them unless
+/// AT2V_ALLOW_EXPERIMENT=1 is set in the process environment)
+pub const AT2V_EXPERIMENT_TAB128: u32 = 1;
+pub const AT2V_EXPERIMENT_COMB_HOT: u32 = 2;
+pub const AT2V_EXPERIMENT_SLOT_WAVES: u32 = 4;
+pub const AT2V_EXPERIMENT_CONST_MSG: u32 = 8;
+pub const AT2V_EXPERIMENT_BCOMB_NOBUILD: u32 = 16;
+
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
 pub const AT2V_SMALL_BATCH_OFF: u32 = 0xffffffff;
 
@@ -131,6 +139,10 @@ pub struct At2vInfo {
     pub cache_built: u64,
     pub cache_build_us: u64,
     pub cache_record_hits: u64,
+    /// AT2V_EXPERIMENT_* bits compiled into the library (0 in a shipped build)
+    pub experiments: u64,
+    /// chunks staged by the host-buffer calls' pipeline
+    pub host_chunks: u64,
 }
 
 /// `Default`: device 0, DALEK_V1, and the library defaults for every size (65536 records, 1 ms, 256 B, depth 3).

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
- * version 6 appended at2v_opts.cpu_threads / flags (num_gpus = 0 now means the CPU batch backend, no device),
+ * version 7 appended at2v_info.experiments / host_chunks (and the AT2V_EXPERIMENT_* bits); version 6 appended at2v_opts.cpu_threads / flags (num_gpus = 0 now means the CPU batch backend, no device),
  * at2v_info.cpu_threads / cpu_batches / cpu_fallbacks / cache_sightings / cache_built / cache_build_us /
  * cache_record_hits,
  * at2v_gen_records_keys_device, at2v_queue_opts.cpu_threads (with the
@@ -35,7 +35,7 @@ extern "C" {
  * at2v_opts.sender_comb and the AT2V_QUEUE_SENDER_COMB queue flag; version 3 appended at2v_opts.sender_cache, at2v_info.gathers / cache_* and the AT2V_E_PEER code (version 2 appended
  * at2v_opts.small_batch_max and at2v_queue_opts.flags). A binding checks at2v_abi_version() == AT2V_ABI_VERSION
  * before passing any struct (the Python and Rust bindings in this repo refuse a mismatching library). */
-#define AT2V_ABI_VERSION 6
+#define AT2V_ABI_VERSION 7
 int at2v_abi_version(void);
 
 typedef struct at2v_ctx at2v_ctx; /* opaque: device(s), streams, scratch, staging buffers, and the RCCL
@@ -98,6 +98,15 @@ enum {
   AT2V_E_PEER = -7      /* at2v_verify_batch_sharded / at2v_comm_init_rank: this rank succeeded but another rank of the
                            communicator failed; that rank's records are verdict 0 (fail closed), discard the batch */
 };
+
+/* Timing-only experiment switches a library may have been compiled with (AT2V_EXP_* build macros; each makes some
+ * verdicts WRONG). at2v_create fails with AT2V_E_INVALID on such a build unless the environment variable
+ * AT2V_ALLOW_EXPERIMENT is "1", and at2v_info.experiments reports the bits. A shipped build has none. */
+#define AT2V_EXPERIMENT_TAB128 1u        /* 128-byte [j]A table entries, the last 8 words dropped */
+#define AT2V_EXPERIMENT_COMB_HOT 2u      /* every A-comb entry read is the same cache line */
+#define AT2V_EXPERIMENT_SLOT_WAVES 4u    /* waves share per-lane table slots */
+#define AT2V_EXPERIMENT_CONST_MSG 8u     /* message words from registers */
+#define AT2V_EXPERIMENT_BCOMB_NOBUILD 16u /* the hit-list kernel's comb of B left unwritten */
 
 /* Create / destroy a context. opts may be NULL (device 0, one GPU, DALEK_V1). Replaces nothing in the
  * reference directly: it owns what drop's SystemManager::run(.., num_cpus::get()) workers did
@@ -198,6 +207,8 @@ typedef struct {
   uint64_t cache_build_us;   /* device time of the build passes that built something (first build block to the flip) */
   uint64_t cache_record_hits;/* records whose sender came from the cache (launches above small_batch_max verify each
                                 record by its own sender's entry, whatever the other records of its chunk) */
+  uint64_t experiments;      /* AT2V_EXPERIMENT_* bits compiled into this library (0 in a shipped build) */
+  uint64_t host_chunks;      /* chunks staged by the host-buffer calls (at2v_verify_batch / _sharded pipeline) */
 } at2v_info;
 /* With a sender cache, at2v_get_info first waits for the context's cache work (its build stream, which follows every
  * cached launch and therefore waits for those launches, and whatever each launch's stream ran before them). */

@@ -10,6 +10,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# The library reads its test / A-B environment hooks (AT2V_TEST_DEVICE_ALIAS, AT2V_TEST_FAIL_LAUNCH, ...) only in a
+# process that sets this gate (csrc/at2v_env.h); the suite is such a process, a production node is not.
+os.environ["AT2V_TEST_HOOKS"] = "1"
 for p in (ROOT, os.path.join(ROOT, "at2-node_amd"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -175,6 +175,21 @@ def test_cpu_fallback_after_device_error(at2v_mod, golden, monkeypatch):
         assert v.info()["cpu_fallbacks"] == 0
 
 
+def test_env_hooks_need_the_gate(at2v_mod, golden, monkeypatch):
+    """VERDICT r5 "Next" 6: the library reads its test hooks only when AT2V_TEST_HOOKS=1 (csrc/at2v_env.h). Without
+    the gate, AT2V_TEST_FAIL_LAUNCH changes nothing: no launch fails, no CPU fallback happens"""
+    monkeypatch.setenv("AT2V_TEST_FAIL_LAUNCH", "1")
+    monkeypatch.delenv("AT2V_TEST_HOOKS")
+    g = golden["adversarial"]
+    with at2v_mod.BatchVerifier(cpu_fallback=True, cpu_threads=2) as v:
+        assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek)
+        assert v.info()["cpu_fallbacks"] == 0
+    monkeypatch.setenv("AT2V_TEST_HOOKS", "1")  # with the gate the hook acts (test_cpu_fallback_after_device_error)
+    with at2v_mod.BatchVerifier(cpu_fallback=True, cpu_threads=2) as v:
+        assert np.array_equal(v.verify_batch(g.pk, g.sig, g.msg, g.off), g.dalek)
+        assert v.info()["cpu_fallbacks"] == 1
+
+
 def test_cpu_fallback_multi_shard(at2v_mod, oracle, monkeypatch):
     """the fallback of an 8-shard context (AT2V_TEST_DEVICE_ALIAS): a failure on one shard re-runs the whole batch on
     the CPU after draining every shard's stream"""

@@ -78,17 +78,21 @@ def test_config1_traffic_every_chunk_hits(at2v_mod, oracle, comb):
 
 @pytest.mark.parametrize("policy", ["dalek", "libsodium"])
 def test_golden_sets_with_cache(at2v_mod, golden, policy, comb):
-    """every golden fixture set, twice (cold, then warm cache), both policies: the small-order, non-canonical and
-    off-curve senders of the adversarial/edge sets are cached with their decode verdicts"""
+    """every golden fixture set, three times (cold: first sightings; second pass: admission claims and builds; third:
+    warm), both policies, with the default admission: the small-order, non-canonical and off-curve senders of the
+    adversarial/edge sets are cached with their decode verdicts and served from the cache (default 20-bit comb of B on
+    the hit list with combs; [j]A tables without) — ADVICE r5: two passes never reached the warm path"""
     # 16,384 keys hold every set's senders (<= 9,200 distinct); with combs that is 16,384 x 1.7 MB = 28 GB of HBM
     with at2v_mod.BatchVerifier(policy=policy, small_batch_max=OFF, sender_cache=1 << 14, sender_comb=comb) as v:
         for name in golden_io.SETS:
             g = golden[name]
             want = g.dalek if policy == "dalek" else g.sodium
-            for rep in range(2):
+            for rep in range(3):
+                h0 = v.info()["cache_record_hits"]
                 got = v.verify_batch(g.pk, g.sig, g.msg, g.off)
                 assert np.array_equal(got, want), (name, rep, np.nonzero(got != want)[0][:10])
-                v.info()  # the next pass finds this pass's keys built
+                hits = v.info()["cache_record_hits"] - h0  # (waits for the build stream: this pass's claims are built)
+            assert hits > 0.9 * g.n, (name, hits, g.n)  # the warm pass: (nearly) every record from the cache
 
 
 def test_repeated_adversarial_senders(at2v_mod, oracle, comb):
@@ -499,7 +503,7 @@ def test_partition_switch_same_verdicts(at2v_mod, golden, monkeypatch, comb, par
             v.info()
 
 
-@pytest.mark.parametrize("wide", [False, True], ids=["bcomb16", "bcomb24"])
+@pytest.mark.parametrize("wide", [False, True], ids=["bcomb20", "bcomb24"])
 def test_comb_hits_staged_and_unstaged_messages(at2v_mod, oracle, wide):
     """The comb hit loop stages a record's message in LDS when every lane's message fits the stage (length up to ~150
     bytes) and ends 8 bytes before the buffer end; any other wave reads word by word (comb2_point_staged returns -1).
@@ -549,3 +553,25 @@ def test_wide_bcomb_golden_sets(at2v_mod, golden, policy):
                     got = v.verify_batch(g.pk, g.sig, g.msg, g.off)
                     assert np.array_equal(got, want), (small, name, rep, np.nonzero(got != want)[0][:10])
                     v.info()
+
+
+def test_host_pipeline_chunks_with_combs(at2v_mod, oracle):
+    """config-1 traffic (64 senders) tiled to 131,072 records, 1,000 of them mutated, through at2v_verify_batch on a comb
+    context: the call stages three chunks (32,832 / 65,664 / 32,576 records), each a cached launch with its own claim
+    slot, builds on the context's stream while the next chunk uploads. Cold, then warm: verdicts equal the oracle's and
+    the warm call serves its records from the combs"""
+    pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
+    reps, L = 32, 48
+    n = 4096 * reps
+    pk, sig, msg = np.tile(pk, (reps, 1)), np.tile(sig, (reps, 1)), np.tile(msg, reps)
+    off = (np.arange(n + 1) * L).astype(np.uint32)
+    pk, sig, msg = _mutate(pk, sig, msg, off, np.random.default_rng(41), 1000, kinds=3)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    assert want.sum() == n - 1000
+    with at2v_mod.BatchVerifier(sender_cache=1024, sender_comb=True) as v:
+        for rep in range(3):
+            h0 = v.info()["cache_record_hits"]
+            got = v.verify_batch(pk, sig, msg, off)
+            assert np.array_equal(got, want), (rep, np.nonzero(got != want)[0][:10])
+            hits = v.info()["cache_record_hits"] - h0
+        assert hits >= n - 64, hits

@@ -291,3 +291,49 @@ def test_config3_total_size_on_one_gpu(at2v_mod):
         assert (int(w_host[-1]) >> (n % 32)) == 0, "pad bits of the last verdict word must be 0"
     finally:
         v.close()
+
+
+# ---- the host-buffer path's chunked pipeline (at2v_api.hip HostPipe; round 6) ----
+# Default context: the first chunk is 32,832 records (one more wave chunk than the low-latency kernel takes), later ones
+# double up to 131,072, and a remainder below the first chunk's size joins the chunk before it. Sizes: one chunk with an
+# absorbed 1-record tail, two chunks (the second ragged), and five chunks (every staging slot reused, the last chunk
+# ragged).
+@pytest.mark.parametrize("n", [32_833, 98_437, 400_009])
+def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, n):
+    """at2v_verify_batch over 1..5 staged chunks, adversarial records, record by record against the oracle; a sentinel
+    word after the bitmap stays untouched and the pad bits of the last word are 0"""
+    pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 101, 0, n, 72)
+    want = oracle.verify_batch(pk, sig, msg, off)
+    lib = at2v_mod.load_library()
+    with at2v_mod.BatchVerifier() as v:
+        for rep in range(2):  # (the second call reuses the staging slots and device buffers of the first)
+            words = np.full((n + 31) // 32 + 1, 0xA5A5A5A5, np.uint32)
+            rc = lib.at2v_verify_batch(v._h, pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, off.ctypes.data, n,
+                                       words.ctypes.data)
+            assert rc == 0
+            assert words[-1] == 0xA5A5A5A5
+            got = at2v_mod.unpack_verdicts(words[:-1], n)
+            assert np.array_equal(got, want), (rep, _mismatch(got, want, cls))
+            if n % 32:
+                assert int(words[(n - 1) // 32]) >> (n % 32) == 0
+
+
+def test_host_pipeline_ragged_messages_regrow(at2v_mod, oracle):
+    """ragged messages (0 B .. 16 KiB) tiled to 100,000 records at an offset msg_off[0] > 0: the chunks carry very
+    different message bytes, so staging slots regrow mid-call; record by record against the oracle"""
+    import ragged_records
+    pk, sig, msg, off, mutated = ragged_records.make(oracle, 2500, seed=20261018)
+    reps = 40
+    n = 2500 * reps
+    pk = np.tile(pk, (reps, 1))
+    sig = np.tile(sig, (reps, 1))
+    lens = np.diff(off.astype(np.int64))
+    msg = np.concatenate([np.zeros(7, np.uint8), np.tile(msg, reps)])
+    offs = np.zeros(n + 1, np.uint32)
+    offs[1:] = np.cumsum(np.tile(lens, reps))
+    offs += 7
+    want = np.tile(oracle.verify_batch(pk[:2500], sig[:2500], msg, offs[:2501]), reps)
+    assert want.sum() == reps * (~mutated).sum()
+    with at2v_mod.BatchVerifier() as v:
+        got = v.verify_batch(pk, sig, msg, offs)
+    assert np.array_equal(got, want), _mismatch(got, want)

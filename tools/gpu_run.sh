@@ -37,6 +37,9 @@ TAG=$1; shift
 D=gpurun_out/$TAG
 mkdir -p $D
 export TMPDIR=/tmp
+# the library's A/B and test hooks (AT2V_SCRATCH_SETS, AT2V_QUEUE_*, ...) act only with this gate (csrc/at2v_env.h); the
+# driver's own bench and test runs do not set it (the suite's conftest does)
+export AT2V_TEST_HOOKS=1
 run() {  # run <name> <seconds> <cmd...>: stdout+stderr to $D/<name>.txt, tail on failure
   local name=$1 t=$2; shift 2
   echo "[gpu_run] $name ($t s): $*"
