@@ -16,10 +16,13 @@
 // context; at2v_verify_shard_gather_device / at2v_verify_batch_sharded verify this rank's index range and
 // ncclAllGather the verdict words over xGMI, so every rank holds the node bitmap (rpc.rs:156-173 consumer).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -38,7 +41,7 @@ namespace at2v {
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
                          const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache,
-                         const PartArgs* part);
+                         const PartArgs* part, int dense);
 size_t btab_bytes();
 hipError_t launch_build_btab(int4* out, hipStream_t stream);
 hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders,
@@ -121,31 +124,42 @@ constexpr int kScratchSets = 2;
 // to the device in chunks through kStageSlots pinned staging buffers, so the three stages of consecutive chunks overlap:
 //   host     the copy pool's threads copy chunk i from the caller's (pageable) arrays into slot i % kStageSlots, packed
 //            as pk | sig | rebased offsets | messages;
-//   copy     one DMA upload per chunk on the shard's copy stream, into the slot's device buffer;
-//   compute  the verify launch of chunk i on compute stream i % 2 (two streams: launch i+1 takes the CUs launch i leaves
-//            during its end-of-launch drain), writing the chunk's verdict words of the shard's device bitmap.
-// Slot reuse is ordered by events: the host refills a pinned buffer once its upload is done (`uploaded`, host wait), the
-// copy stream overwrites a device buffer once the launch that read it is done (`consumed`, device wait). The first chunk
-// is small (it is the pipeline's fill: nothing runs on the device until it is up), later ones double up to
-// kStageMaxRecords. Round 1 measured the previous form of this call (pageable hipMemcpyAsync, then verify, then D2H) at
-// 54 M/s against a 78 M/s kernel; the stages were serial.
+//   copy     DMA uploads on the shard's copy stream into the chunk's own region of the pipe's device arena;
+//   compute  the verify launch of chunk i on compute stream i % 2 (two streams on two hardware queues: launch i+1 takes
+//            the CUs launch i leaves during its end-of-launch drain), writing the chunk's verdict words of the shard's
+//            device bitmap; dense grids (whole CUs per block), so small chunks run at full rate beside each other.
+// The host refills a pinned slot once its upload is done (`uploaded`, host wait). The first two chunks are half a device
+// each (the pipeline's fill: nothing runs until the first is up), later ones kStageMaxRecords, one full round of the
+// persistent grid. Splitting a batch into such launches costs nothing on the device (1M records as 8 launches of 131,072:
+// 9.30 ms on two streams against 9.34 ms for one launch, profiles/r06j). Round 1 measured the previous form of this call
+// (pageable hipMemcpyAsync, then verify, then D2H) at 54 M/s against a 78 M/s kernel; the stages were serial.
 constexpr int kStageSlots = 3;
 constexpr size_t kStageMaxRecords = 131072;  // 2,048 wave chunks: one per resident wave of the persistent grid
-constexpr size_t kStageFirstRecords = 32768;
+constexpr size_t kStageFirstRecords = 65536;  // 1,024 wave chunks: half the device in dense blocks
 constexpr size_t kCopyPiece = 1 << 20;       // bytes per copy-pool job item
 constexpr size_t kCopyPoolMin = 2 << 20;     // chunks below this many bytes are copied by the calling thread alone
+struct ChunkLaunch {  // a staged chunk's launch: where its parts are on the device, where its verdict words go
+  uint8_t* d = nullptr;
+  size_t sig = 0, off = 0, msg = 0, mb = 0, c = 0;
+  uint32_t* d_words = nullptr;
+  bool throughput = false;
+  int slot = 0, stream = 0;
+};
 struct StageSlot {
   uint8_t* host = nullptr;  // pinned
   size_t host_cap = 0;
-  DevBuf dev;
-  hipEvent_t uploaded = nullptr;  // copy stream, after the slot's last upload: the host may refill `host`
-  hipEvent_t consumed = nullptr;  // compute stream, after the last launch that read `dev`: the copy stream may refill it
+  hsa_signal_t uploaded{0};  // the slot's DMA uploads: set to their count, each decrements it as it completes
 };
 struct HostPipe {
-  hipStream_t copy = nullptr;                 // uploads, the verdict download, (sharded) the all-gathers
+  hipStream_t copy = nullptr;                 // the verdict download, (sharded) the all-gathers
   hipStream_t comp[2] = {nullptr, nullptr};   // verify launches of the chunks, alternating
   hipEvent_t comp_done[2] = {nullptr, nullptr};
   StageSlot slot[kStageSlots];
+  DevBuf arena;         // a call's chunks on the device, each in its own region (arena_at: the next free byte)
+  size_t arena_at = 0;
+  hsa_agent_t gpu{0}, cpu{0};  // the DMA uploads' destination and source agents
+  bool pending = false;  // a chunk whose uploads are submitted and whose launch is not issued yet
+  ChunkLaunch pend;
   uint64_t chunks = 0;  // chunks issued by this shard (slot chunks % kStageSlots, compute stream chunks % 2)
 };
 
@@ -185,6 +199,9 @@ struct at2v_ctx {
   // the host-buffer path's chunk schedule (HostPipe; test hooks AT2V_TEST_STAGE_FIRST / _MAX / AT2V_TEST_COPY_THREADS)
   size_t stage_first = kStageFirstRecords, stage_max = kStageMaxRecords;
   unsigned copy_threads = 8;
+  int pipe_streams = 1;     // create_comp_stream mode (test hook AT2V_TEST_PIPE_STREAMS)
+  bool pipe_trace = false;  // test hook AT2V_TEST_PIPE_TRACE: per host-buffer call, where the host's time went (stderr)
+  double tr_wait = 0, tr_copy = 0, tr_enq = 0;  // seconds, this call
   uint64_t host_chunks = 0;  // chunks staged by host-buffer calls (at2v_info.host_chunks)
   uint32_t test_fail_launches = 0;  // AT2V_TEST_FAIL_LAUNCH (tests only): that many launches fail before the kernel
   bool partition = true;  // cached launches above pair_max classify, then verify hits and misses apart (AT2V_CACHE_PARTITION)
@@ -464,7 +481,10 @@ hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
 // after a compaction waits for it (cache_before_launch). The verdict words are zeroed first (fail closed).
 hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                         uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream,
-                        bool zero_verdicts = true) {
+                        bool zero_verdicts = true, bool pipeline = false) {
+  // a chunk of the host-buffer pipeline whose batch is above small_batch_max: the throughput kernels at every chunk
+  // size, with dense grids (launch_verify)
+  const uint32_t pair_max = pipeline ? 0u : ctx->pair_max;
   if (ctx->test_fail_launches) {  // test hook: a launch failure, as a faulting device would report it
     --ctx->test_fail_launches;
     return hipErrorLaunchFailure;
@@ -472,10 +492,10 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   const int j = (int)(s.next_set++ % (unsigned)s.sets);
   hipError_t e = hipStreamWaitEvent(stream, s.scratch_free[j], 0);
   // the cache serves the throughput kernel (launches above small_batch_max records; with combs, every launch)
-  SenderCache* c = (s.cache && (n > ctx->pair_max || s.cache->args.comb)) ? s.cache : nullptr;
+  SenderCache* c = (s.cache && (n > pair_max || s.cache->args.comb)) ? s.cache : nullptr;
   // the four-wave comb kernel of small batches writes every verdict word of the launch whatever the verdicts (its
   // blocks stride over all chunks), so the zeroing is left out there: one dependent memset less on the latency path
-  if (c && c->args.comb && n <= ctx->pair_max) zero_verdicts = false;
+  if (c && c->args.comb && n <= pair_max) zero_verdicts = false;
   if (e == hipSuccess && zero_verdicts) e = hipMemsetAsync(verdicts, 0, ((size_t)n + 31) / 32 * 4, stream);
   const int cs = c ? (int)(c->launches % kClaimSlots) : 0;
   if (e == hipSuccess && c) e = cache_before_launch(*c, s, stream, cs);
@@ -487,7 +507,7 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
     ca = c->args;
   }
   at2v::PartArgs pa{};
-  const bool part = c && ctx->partition && n > ctx->pair_max;
+  const bool part = c && ctx->partition && n > pair_max;
   if (e == hipSuccess && part) {
     const size_t need = (size_t)n * at2v::part_bytes_per_record();
     if (s.part[j].cap < need) {  // grows: the set's previous launch (it reads the old lists) must be done first
@@ -499,8 +519,8 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   }
   if (e == hipSuccess)
     e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch[j].p,
-                            (const int4*)s.btab.p, s.grid, ctx->pair_max, stream, c ? &ca : nullptr,
-                            part ? &pa : nullptr);
+                            (const int4*)s.btab.p, s.grid, pair_max, stream, c ? &ca : nullptr,
+                            part ? &pa : nullptr, pipeline ? 1 : 0);
   if (e == hipSuccess && c) {
     // claims of this launch -> payloads on the build stream (later launches use them; this one did not wait)
     e = hipEventRecord(c->claims_ready[cs], stream);
@@ -515,14 +535,16 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
 void free_pipe(Shard& s) {
   HostPipe* p = s.pipe;
   if (!p) return;
+  for (StageSlot& sl : p->slot)  // (uploads still in flight: a call that failed between submit and launch)
+    if (sl.uploaded.handle)
+      (void)hsa_signal_wait_scacquire(sl.uploaded, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
   for (hipStream_t st : {p->copy, p->comp[0], p->comp[1]})
     if (st) (void)hipStreamSynchronize(st);
   for (StageSlot& sl : p->slot) {
     if (sl.host) (void)hipHostFree(sl.host);
-    sl.dev.release();
-    for (hipEvent_t ev : {sl.uploaded, sl.consumed})
-      if (ev) (void)hipEventDestroy(ev);
+    if (sl.uploaded.handle) (void)hsa_signal_destroy(sl.uploaded);
   }
+  p->arena.release();
   for (hipEvent_t ev : p->comp_done)
     if (ev) (void)hipEventDestroy(ev);
   for (hipStream_t st : {p->copy, p->comp[0], p->comp[1]})
@@ -531,24 +553,66 @@ void free_pipe(Shard& s) {
   s.pipe = nullptr;
 }
 
+hipError_t hsa_err(hsa_status_t st) { return st == HSA_STATUS_SUCCESS ? hipSuccess : hipErrorUnknown; }
+
+hsa_status_t find_cpu_agent(hsa_agent_t a, void* data) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(data) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// A compute stream of the pipe. The two must sit on different hardware queues, or their launches run one after the
+// other and every chunk pays its own end-of-launch drain: HIP maps streams onto GPU_MAX_HW_QUEUES (4) shared queues, and
+// in a process with a few streams already the two new ones landed on the same queue (profiles/r06d: queue 4 for both).
+// mode 0: plain streams; 1: the second one at the highest priority (a queue of its own priority level); 2: streams with
+// a full CU mask (HIP gives a CU-masked stream a queue of its own). Test hook AT2V_TEST_PIPE_STREAMS.
+hipError_t create_comp_stream(hipStream_t* st, int j, int mode, int device) {
+  if (mode == 1 && j == 1) {
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    return e == hipSuccess ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest) : e;
+  }
+  if (mode == 2) {
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> mask((size_t)(prop.multiProcessorCount + 31) / 32, 0xffffffffu);
+    return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+  }
+  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 // the shard's pipe (current device = s.device); its events are recorded once, so the first waits are no-ops
-hipError_t ensure_pipe(Shard& s) {
+hipError_t ensure_pipe(Shard& s, int mode) {
   if (s.pipe) return hipSuccess;
   HostPipe* p = new (std::nothrow) HostPipe;
   if (!p) return hipErrorOutOfMemory;
   s.pipe = p;
   hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
   for (int j = 0; j < 2 && e == hipSuccess; ++j) {
-    e = hipStreamCreateWithFlags(&p->comp[j], hipStreamNonBlocking);
+    e = create_comp_stream(&p->comp[j], j, mode, s.device);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->comp_done[j], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(p->comp_done[j], p->copy);
   }
-  for (StageSlot& sl : p->slot) {
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.uploaded, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(sl.uploaded, p->copy);
-    if (e == hipSuccess) e = hipEventRecord(sl.consumed, p->copy);
+  // The uploads go to the DMA engines through HSA directly (a host-to-device hsa_amd_memory_async_copy runs on an SDMA
+  // engine): HIP's hipMemcpyAsync handed some of them to blit kernels, which take CUs from the running verify launches
+  // and delay the next one (profiles/r06k, r06m: 1.25 ms for a 13 MB upload beside a launch, against 0.23 ms on SDMA).
+  // HIP already initialised the runtime; hsa_init only takes a reference.
+  if (e == hipSuccess) e = hsa_err(hsa_init());
+  if (e == hipSuccess) {
+    hsa_amd_pointer_info_t info;
+    std::memset(&info, 0, sizeof info);
+    info.size = sizeof info;
+    e = hsa_err(hsa_amd_pointer_info(s.btab.p, &info, nullptr, nullptr, nullptr));
+    if (e == hipSuccess) p->gpu = info.agentOwner;
+    if (e == hipSuccess && (hsa_iterate_agents(find_cpu_agent, &p->cpu) != HSA_STATUS_INFO_BREAK || !p->cpu.handle))
+      e = hipErrorUnknown;
   }
+  for (StageSlot& sl : p->slot)
+    if (e == hipSuccess) e = hsa_err(hsa_signal_create(0, 0, nullptr, &sl.uploaded));
   if (e != hipSuccess) free_pipe(s);
   return e;
 }
@@ -603,62 +667,140 @@ struct CopyJob {
 // the chunk owns whole verdict words) -> staging slot -> device -> verify launch writing d_words (the chunk's words of
 // the shard's device bitmap, zeroed by the launch first). Current device = s.device. Returns after the launch is
 // enqueued; the host waits only for the slot's previous upload (and, when the slot must grow, for its previous launch).
-hipError_t issue_chunk(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, const uint8_t* pk, const uint8_t* sig,
-                       const uint8_t* msg, const uint32_t* msg_off, size_t a, size_t c, uint32_t* d_words) {
-  HostPipe& p = *s.pipe;
-  StageSlot& sl = p.slot[p.chunks % kStageSlots];
-  const int j = (int)(p.chunks % 2);
-  const uint32_t mb0 = msg_off[a];
-  const size_t mb = (size_t)(msg_off[a + c] - mb0);
-  const ChunkLayout L = chunk_layout(c, mb);
-  hipError_t e = hipEventSynchronize(sl.uploaded);
-  if (e == hipSuccess && (sl.host_cap < L.total || sl.dev.cap < L.total)) {
-    e = hipEventSynchronize(sl.consumed);  // (the slot's device buffer is freed by a regrow)
-    if (e == hipSuccess && sl.host_cap < L.total) {
-      if (sl.host) (void)hipHostFree(sl.host);
-      sl.host = nullptr;
-      sl.host_cap = 0;
-      const size_t want = std::max(L.total + L.total / 4, chunk_layout(ctx->stage_max, 0).total);
-      e = hipHostMalloc((void**)&sl.host, want, hipHostMallocDefault);
-      if (e == hipSuccess) sl.host_cap = want;
-    }
-    if (e == hipSuccess) e = sl.dev.ensure(std::max(L.total, sl.host_cap));
-  }
-  if (e != hipSuccess) return e;
-  CopyJob job;
-  job.add(sl.host, pk + a * 32, c * 32);
-  job.add(sl.host + L.sig, sig + a * 64, c * 64);
-  job.add_offsets((uint32_t*)(sl.host + L.off), msg_off + a, c + 1, mb0);
-  if (mb) job.add(sl.host + L.msg, msg + mb0, mb);
-  if (copier && L.upload >= kCopyPoolMin) {
+// Host copy of one job (the copy pool's threads for large ones, the calling thread for small ones).
+void run_copy(at2v::CpuPool* copier, CopyJob& job, size_t bytes) {
+  if (copier && bytes >= kCopyPoolMin) {
     at2v::pool_run(copier, job.pieces.size(), CopyJob::run_piece, &job);
   } else {
     for (size_t i = 0; i < job.pieces.size(); ++i) CopyJob::run_piece(&job, i);
   }
-  uint8_t* d = (uint8_t*)sl.dev.p;
-  e = hipStreamWaitEvent(p.copy, sl.consumed, 0);
-  if (e == hipSuccess) e = hipMemcpyAsync(d, sl.host, L.upload, hipMemcpyHostToDevice, p.copy);
-  if (e == hipSuccess) e = hipEventRecord(sl.uploaded, p.copy);
-  if (e == hipSuccess) e = hipStreamWaitEvent(p.comp[j], sl.uploaded, 0);
+  job.pieces.clear();
+}
+
+// device bytes a shard's part of a host batch takes in the pipe's arena: every chunk's layout, 256-aligned
+size_t arena_bytes(size_t m, size_t mb, size_t first) {
+  const size_t chunks = m / (first ? first : 1) + 2;
+  return m * 100 + mb + chunks * (16 + 4 + 16 + 256) + 256;
+}
+
+// wait for a slot's uploads (an SDMA error leaves the signal negative)
+hipError_t wait_uploads(StageSlot& sl) {
+  const hsa_signal_value_t v =
+      hsa_signal_wait_scacquire(sl.uploaded, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+  if (v == 0) return hipSuccess;
+  hsa_signal_store_screlease(sl.uploaded, 0);  // (reported once; the slot starts clean for the next call)
+  return hipErrorUnknown;
+}
+
+// The launch of the shard's pending chunk (current device = s.device), once its uploads are done: the launch needs no
+// device-side dependency on the copies, so the verify kernels run back to back on the compute streams while the host
+// stages the next chunks.
+hipError_t flush_chunk(at2v_ctx* ctx, Shard& s) {
+  HostPipe& p = *s.pipe;
+  if (!p.pending) return hipSuccess;
+  p.pending = false;
+  const ChunkLaunch& k = p.pend;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  hipError_t e = wait_uploads(p.slot[k.slot]);
+  if (ctx->pipe_trace) ctx->tr_wait += std::chrono::duration<double>(clk::now() - t0).count();
   if (e == hipSuccess)
-    e = launch_shard(ctx, s, d, d + L.sig, d + L.msg, (uint32_t)mb, (const uint32_t*)(d + L.off), (uint32_t)c, d_words,
-                     p.comp[j]);
-  if (e == hipSuccess) e = hipEventRecord(sl.consumed, p.comp[j]);
-  if (e == hipSuccess) e = hipEventRecord(p.comp_done[j], p.comp[j]);
-  ++p.chunks;
-  ++ctx->host_chunks;
+    e = launch_shard(ctx, s, k.d, k.d + k.sig, k.d + k.msg, (uint32_t)k.mb, (const uint32_t*)(k.d + k.off),
+                     (uint32_t)k.c, k.d_words, p.comp[k.stream], true, k.throughput);
+  if (e == hipSuccess) e = hipEventRecord(p.comp_done[k.stream], p.comp[k.stream]);
   return e;
 }
 
-// The chunk schedule of one shard's part of a host batch: kStageFirstRecords (or, if larger, one wave chunk more than
-// the low-latency kernel takes), doubling up to kStageMaxRecords; a remainder smaller than the first chunk joins the
-// chunk before it. Every chunk but the last is a multiple of 64 records.
+// Records [a, a + c) of the caller's batch (absolute indices; a multiple of 64 relative to the shard's first record, so
+// the chunk owns whole verdict words): staging slot -> DMA uploads into the chunk's own region of the pipe's device
+// arena -> (the next call of this function, or flush_chunk) verify launch writing d_words (the chunk's words of the
+// shard's device bitmap, zeroed by the launch first). Current device = s.device. The four parts (pk, sig + offsets,
+// messages) are copied and submitted one after the other, so the DMA of one overlaps the host copy of the next; then the
+// previous chunk is launched (its uploads had this chunk's host copy to finish). The first chunk of a call (`first`)
+// is launched at once: it is the pipeline's fill.
+hipError_t issue_chunk(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, const uint8_t* pk, const uint8_t* sig,
+                       const uint8_t* msg, const uint32_t* msg_off, size_t a, size_t c, uint32_t* d_words,
+                       bool throughput, bool first) {
+  HostPipe& p = *s.pipe;
+  const int k = (int)(p.chunks % kStageSlots);
+  StageSlot& sl = p.slot[k];
+  const uint32_t mb0 = msg_off[a];
+  const size_t mb = (size_t)(msg_off[a + c] - mb0);
+  const ChunkLayout L = chunk_layout(c, mb);
+  if (p.arena_at + L.total > p.arena.cap) return hipErrorInvalidValue;  // (sized by the caller: cannot happen)
+  uint8_t* d = (uint8_t*)p.arena.p + p.arena_at;
+  p.arena_at += (L.total + 255) & ~(size_t)255;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  hipError_t e = wait_uploads(sl);  // (done already: the slot's chunk was launched, which waited for them)
+  if (e == hipSuccess && sl.host_cap < L.total) {
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.host = nullptr;
+    sl.host_cap = 0;
+    const size_t want = std::max(L.total + L.total / 4, chunk_layout(ctx->stage_max, 0).total);
+    e = hipHostMalloc((void**)&sl.host, want, hipHostMallocDefault);
+    if (e == hipSuccess) sl.host_cap = want;
+  }
+  if (e != hipSuccess) return e;
+  const auto t1 = clk::now();
+  hsa_signal_store_screlease(sl.uploaded, mb ? 3 : 2);  // the parts below, each decrements it when done
+  auto upload = [&](size_t at, size_t len) {
+    return hsa_err(hsa_amd_memory_async_copy(d + at, p.gpu, sl.host + at, p.cpu, len, 0, nullptr, sl.uploaded));
+  };
+  CopyJob job;
+  job.add(sl.host, pk + a * 32, c * 32);
+  run_copy(copier, job, c * 32);
+  e = upload(0, c * 32);
+  job.add(sl.host + L.sig, sig + a * 64, c * 64);
+  job.add_offsets((uint32_t*)(sl.host + L.off), msg_off + a, c + 1, mb0);
+  run_copy(copier, job, c * 68);
+  if (e == hipSuccess) e = upload(L.sig, L.msg - L.sig);
+  if (mb) {
+    job.add(sl.host + L.msg, msg + mb0, mb);
+    run_copy(copier, job, mb);
+    if (e == hipSuccess) e = upload(L.msg, mb);
+  }
+  if (e != hipSuccess) {  // (a submit failed: nothing waits for this slot's parts any more; the call fails)
+    hsa_signal_store_screlease(sl.uploaded, 0);
+    return e;
+  }
+  const auto t2 = clk::now();
+  e = flush_chunk(ctx, s);
+  p.pend = ChunkLaunch{d, L.sig, L.off, L.msg, mb, c, d_words, throughput, k, (int)(p.chunks % 2)};
+  p.pending = true;
+  if (e == hipSuccess && first) e = flush_chunk(ctx, s);
+  ++p.chunks;
+  ++ctx->host_chunks;
+  if (ctx->pipe_trace) {
+    const auto t3 = clk::now();
+    ctx->tr_wait += std::chrono::duration<double>(t1 - t0).count();
+    ctx->tr_copy += std::chrono::duration<double>(t2 - t1).count();
+    ctx->tr_enq += std::chrono::duration<double>(t3 - t2).count();
+  }
+  return e;
+}
+
+// The pipe's arena for a shard's part of a call (m records, mb message bytes), before its first chunk: every launch of
+// the previous host-buffer call has completed (the call waited for its verdict copy, which followed them).
+hipError_t begin_arena(at2v_ctx* ctx, Shard& s, size_t m, size_t mb) {
+  HostPipe& p = *s.pipe;
+  for (StageSlot& sl : p.slot) (void)wait_uploads(sl);  // (after a failed call, uploads may still write the arena)
+  p.pending = false;
+  p.arena_at = 0;
+  return p.arena.ensure(arena_bytes(m, mb, std::min(ctx->stage_first, std::max<size_t>(m, 1))));
+}
+
+// The chunk schedule of one shard's part of a host batch: a part the low-latency kernel takes whole (<= small_batch_max
+// records) is one chunk; a larger one starts with kStageFirstRecords (the pipeline's fill: nothing runs on the device until
+// it is up), then doubles up to kStageMaxRecords, and a remainder smaller than the first chunk joins the chunk before
+// it. Those chunks run the throughput kernels with dense grids whatever their size (launch_shard `pipeline`). Every
+// chunk but the last is a multiple of 64 records.
 struct ChunkPlan {
   size_t first = 0, next = 0, pos = 0, m = 0, cap = 0;
   void init(size_t m_, const at2v_ctx* ctx) {
     m = m_;
     pos = 0;
-    first = std::max(ctx->stage_first, ((size_t)ctx->pair_max + 64) / 64 * 64);
+    first = m <= ctx->pair_max ? std::max<size_t>(m, 64) : ctx->stage_first;
     cap = std::max(ctx->stage_max, first);
     next = first;
   }
@@ -666,7 +808,7 @@ struct ChunkPlan {
   size_t take() {  // the next chunk's record count (its first record is pos before the call)
     size_t c = std::min(next, m - pos);
     if (m - pos - c < first) c = m - pos;
-    next = std::min(next * 2, cap);
+    if (pos > 0 || first >= cap) next = std::min(next * 2, cap);  // (the first size twice: two launches fill the device)
     pos += c;
     return c;
   }
@@ -775,6 +917,8 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   c->stage_first = (size_t)at2v::test_env_long("AT2V_TEST_STAGE_FIRST", (long)kStageFirstRecords) / 64 * 64;
   c->stage_max = (size_t)at2v::test_env_long("AT2V_TEST_STAGE_MAX", (long)kStageMaxRecords) / 64 * 64;
   c->copy_threads = (unsigned)at2v::test_env_long("AT2V_TEST_COPY_THREADS", 8);
+  c->pipe_streams = (int)at2v::test_env_long("AT2V_TEST_PIPE_STREAMS", c->pipe_streams);
+  c->pipe_trace = at2v::test_env_long("AT2V_TEST_PIPE_TRACE", 0) != 0;
   if (c->stage_first < 64) c->stage_first = 64;
   if (c->stage_max < c->stage_first) c->stage_max = c->stage_first;
   c->pair_max = o.small_batch_max == 0 ? AT2V_SMALL_BATCH_DEFAULT
@@ -885,9 +1029,12 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     if (r.size() == 0) continue;
     hipError_t e = hipSetDevice(s.device);
     if (e == hipSuccess) e = s.verdict.ensure(((r.size() + 31) / 32) * 4);
-    if (e == hipSuccess) e = ensure_pipe(s);
+    if (e == hipSuccess) e = ensure_pipe(s, ctx->pipe_streams);
+    if (e == hipSuccess) e = begin_arena(ctx, s, r.size(), (size_t)(msg_off[r.hi] - msg_off[r.lo]));
     err[g] = e;
   }
+  const auto tc0 = std::chrono::steady_clock::now();
+  ctx->tr_wait = ctx->tr_copy = ctx->tr_enq = 0;
   for (bool more = true; more;) {
     more = false;
     for (size_t g = 0; g < G; ++g) {
@@ -897,9 +1044,17 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
       const size_t at = cp.pos, c = cp.take();
       err[g] = hipSetDevice(s.device);
       if (err[g] == hipSuccess)
-        err[g] = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, lo[g] + at, c, (uint32_t*)s.verdict.p + at / 32);
+        err[g] = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, lo[g] + at, c, (uint32_t*)s.verdict.p + at / 32,
+                             cp.m > ctx->pair_max, at == 0);
       more = more || !cp.done();
     }
+  }
+  for (size_t g = 0; g < G; ++g) {  // the last chunk of every shard
+    Shard& s = ctx->shards[g];
+    if (plan[g].m == 0 || !s.pipe) continue;
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = flush_chunk(ctx, s);
+    if (err[g] == hipSuccess) err[g] = e;
   }
   // the verdict words of each shard, once its last two launches are done (copy stream)
   for (size_t g = 0; g < G; ++g) {
@@ -923,6 +1078,10 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     hipError_t e = hipEventSynchronize(s.copied);
     if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
+  if (ctx->pipe_trace)
+    std::fprintf(stderr, "[at2v pipe] n %zu: %.3f ms (host: wait %.3f, copy %.3f, enqueue %.3f ms)\n", n,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - tc0).count() * 1e3, ctx->tr_wait * 1e3,
+                 ctx->tr_copy * 1e3, ctx->tr_enq * 1e3);
   if (rc != AT2V_OK && ctx->cpu) {
     // AT2V_CTX_CPU_FALLBACK: the records are still in the caller's host buffers. Drain what the shards enqueued (no
     // verdict copy of this call may land after the CPU's words), then verify the whole batch on the CPU backend.
@@ -1063,19 +1222,23 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
   // learns of it. The collectives run on the pipe's copy stream (the context's own stream if the pipe could not be made),
   // behind the chunks' launches; the sender cache's builds run on the context's stream and do not delay them.
   if (e == hipSuccess) e = s.verdict.ensure(wpr * 4);
-  if (e == hipSuccess) e = ensure_pipe(s);
+  if (e == hipSuccess) e = ensure_pipe(s, ctx->pipe_streams);
   hipStream_t st = s.pipe ? s.pipe->copy : s.stream;
   const size_t used = (m + 31) / 32;  // words the chunks' launches write (each zeroes its own first)
   if (e == hipSuccess && used < wpr)
     e = hipMemsetAsync((uint32_t*)s.verdict.p + used, 0, (wpr - used) * 4, st);  // pad words (an empty rank: all)
+  if (e == hipSuccess && m) e = begin_arena(ctx, s, m, (size_t)(msg_off[a + m] - msg_off[a]));
   if (e == hipSuccess && m) {
     at2v::CpuPool* copier = copy_pool(ctx);
     ChunkPlan cp;
     cp.init(m, ctx);
     while (e == hipSuccess && !cp.done()) {
       const size_t at = cp.pos, c = cp.take();
-      e = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, a + at, c, (uint32_t*)s.verdict.p + at / 32);
+      e = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, a + at, c, (uint32_t*)s.verdict.p + at / 32,
+                      m > ctx->pair_max, at == 0);
     }
+    const hipError_t ef = flush_chunk(ctx, s);  // the last chunk
+    if (e == hipSuccess) e = ef;
     for (int j = 0; j < 2 && e == hipSuccess; ++j) e = hipStreamWaitEvent(st, s.pipe->comp_done[j], 0);
   }
   int rc = hip_code(e);

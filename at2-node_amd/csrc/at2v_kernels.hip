@@ -2842,7 +2842,7 @@ size_t part_bytes_per_record() { return 12; }  // hidx, hinfo, midx
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
                          const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache,
-                         const PartArgs* part) {
+                         const PartArgs* part, int dense) {
   if (n == 0) return hipSuccess;
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
   if (n <= pair_max && !(cache && cache->comb)) {  // (with combs, small batches take the comb kernel: faster still)
@@ -2857,7 +2857,12 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   }
 #endif
   const uint32_t nchunks = (n + 63) / 64;
-  const uint32_t need_blocks = (nchunks + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);  // half-filled blocks
+  // Blocks: a launch below the full grid spreads its chunks over twice as many blocks, half filled (one wave per SIMD:
+  // the lowest latency for a lone batch); `dense` (the host-buffer pipeline's chunk launches, at2v_api.hip HostPipe)
+  // fills every block, so a small launch takes few whole CUs at full rate and leaves the rest to the launch beside it
+  // (1M records as 16 launches of 65,536: 13.3 ms half filled, one stream; profiles/r06i)
+  const uint32_t per_block = dense ? kWavesPerBlock : kWavesPerBlock / 2;
+  const uint32_t need_blocks = (nchunks + per_block - 1) / per_block;
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
   // chunk queue counter: the word after the `grid` blocks' lane slots (scratch_bytes(grid)); the four-wave comb kernel of
   // small batches strides over its chunks and needs none (one dependent memset less on the latency path)

@@ -56,7 +56,7 @@ def test_experiment_build_refuses_contexts(tmp_path):
     subprocess.run(hip + ["-DAT2V_EXP_BCOMB_NOBUILD=1", "-c", os.path.join(CSRC, "at2v_api.hip"), "-o", str(api)],
                    check=True, timeout=600)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", str(api), *OBJS,
-                    "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", str(lib)], check=True, timeout=300)
+                    "-L/opt/rocm/lib", "-lrccl", "-lhsa-runtime64", "-Wl,-rpath,/opt/rocm/lib", "-o", str(lib)], check=True, timeout=300)
     env = {k: v for k, v in os.environ.items() if k != "AT2V_ALLOW_EXPERIMENT"}
     rc, _ = _probe(str(lib), env)
     assert rc == -1, "an experiment build must refuse contexts (AT2V_E_INVALID)"

@@ -557,8 +557,8 @@ def test_wide_bcomb_golden_sets(at2v_mod, golden, policy):
 
 def test_host_pipeline_chunks_with_combs(at2v_mod, oracle):
     """config-1 traffic (64 senders) tiled to 131,072 records, 1,000 of them mutated, through at2v_verify_batch on a comb
-    context: the call stages three chunks (32,832 / 65,664 / 32,576 records), each a cached launch with its own claim
-    slot, builds on the context's stream while the next chunk uploads. Cold, then warm: verdicts equal the oracle's and
+    context: the call stages four chunks (16,384 / 32,768 / 65,536 / 16,384 records), each a cached launch with its own
+    claim slot, builds on the context's stream while the next chunk uploads. Cold, then warm: verdicts equal the oracle's and
     the warm call serves its records from the combs"""
     pk, sig, msg, off, snd, seq = oracle.gen_at2_transactions()
     reps, L = 32, 48

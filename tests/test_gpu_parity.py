@@ -298,10 +298,14 @@ def test_config3_total_size_on_one_gpu(at2v_mod):
 # double up to 131,072, and a remainder below the first chunk's size joins the chunk before it. Sizes: one chunk with an
 # absorbed 1-record tail, two chunks (the second ragged), and five chunks (every staging slot reused, the last chunk
 # ragged).
+@pytest.mark.parametrize("streams", ["plain", "priority", "cumask"])
 @pytest.mark.parametrize("n", [32_833, 98_437, 400_009])
-def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, n):
-    """at2v_verify_batch over 1..5 staged chunks, adversarial records, record by record against the oracle; a sentinel
-    word after the bitmap stays untouched and the pad bits of the last word are 0"""
+def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, monkeypatch, n, streams):
+    """at2v_verify_batch through the chunked pipeline (16,384 records, doubling to 131,072, dense grids; 1..6 chunks,
+    every staging slot reused), with its two compute streams created each way (test hook AT2V_TEST_PIPE_STREAMS: on one
+    hardware queue or two, so consecutive chunk launches overlap or not). Adversarial records, record by record against
+    the oracle; a sentinel word after the bitmap stays untouched and the pad bits of the last word are 0"""
+    monkeypatch.setenv("AT2V_TEST_PIPE_STREAMS", {"plain": "0", "priority": "1", "cumask": "2"}[streams])
     pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 101, 0, n, 72)
     want = oracle.verify_batch(pk, sig, msg, off)
     lib = at2v_mod.load_library()
