@@ -115,6 +115,13 @@ struct SenderCache {
   bool compact_pending = false;  // a launch found the cache full: compact before a later launch
   bool compacting = false;       // a compaction is enqueued on the build stream and has not been swapped in yet
   uint64_t launches = 0;  // launch epochs (entries record the last launch that used them)
+  // Thrash guard (round 6, VERDICT r5 "Next" 2): a compaction that had to evict entries used by the latest launch
+  // (its age threshold is 0: the working set is larger than the cache and every cached key is still in use) would only
+  // trade comb builds for other keys of the same worth. The cache then stops claiming for freeze_len launches (8,
+  // doubling up to 256 while compactions keep cutting at age 0; a compaction that cuts older entries resets it), so the
+  // keys it holds keep serving and no build is spent on churn.
+  uint64_t compactions_seen = 0;
+  uint32_t freeze_len = 0, freeze_left = 0;
 };
 
 // scratch sets per device (AT2V_SCRATCH_SETS overrides, 1..4; 1 = every launch waits for the previous one)
@@ -423,7 +430,16 @@ hipError_t cache_before_launch(SenderCache& c, Shard& s, hipStream_t stream, int
   hipError_t e = hipStreamWaitEvent(stream, c.slot_free[j], 0);
   if (e == hipSuccess && c.copy_pending && hipEventQuery(c.ctl_copied) == hipSuccess) {
     c.copy_pending = false;
-    if (c.host_ctl[at2v::kCtlFull]) c.compact_pending = true;
+    if (c.host_ctl[at2v::kCtlCompactions] > c.compactions_seen) {  // a compaction has run since the last look
+      c.compactions_seen = c.host_ctl[at2v::kCtlCompactions];
+      if (c.host_ctl[at2v::kCtlThreshold] == 0) {
+        c.freeze_len = c.freeze_len ? std::min<uint32_t>(2 * c.freeze_len, 256) : 8;
+        c.freeze_left = c.freeze_len;
+      } else {
+        c.freeze_len = 0;
+      }
+    }
+    if (c.host_ctl[at2v::kCtlFull] && !c.freeze_left) c.compact_pending = true;
   }
   auto wait_all_launches = [&](hipStream_t st) {  // every launch so far: the last one on each scratch set
     hipError_t r = hipSuccess;
@@ -451,7 +467,8 @@ hipError_t cache_before_launch(SenderCache& c, Shard& s, hipStream_t stream, int
       c.compact_pending = false;
     }
   }
-  c.args.no_claim = c.compacting ? 1 : 0;
+  c.args.no_claim = c.compacting || c.freeze_left ? 1 : 0;
+  if (c.freeze_left) --c.freeze_left;
   return e;
 }
 
