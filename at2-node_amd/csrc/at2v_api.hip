@@ -40,9 +40,11 @@
 namespace at2v {
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache,
-                         const PartArgs* part, int dense);
+                         const int4* btab, const int4* btab24, int grid, uint32_t pair_max, hipStream_t stream,
+                         const CacheArgs* cache, const PartArgs* part, int dense, const StagedArgs* staged);
 size_t btab_bytes();
+size_t ladder_btab_bytes();
+hipError_t launch_build_ladder_btab(int4* out, void* scratch, hipStream_t stream);
 hipError_t launch_build_btab(int4* out, hipStream_t stream);
 hipError_t launch_gen(uint64_t cfg, uint64_t first, uint32_t n, uint32_t msg_len, uint64_t senders,
                       const uint64_t* keys, uint8_t* pk, uint8_t* sig, uint8_t* msg, uint32_t* off, hipStream_t stream);
@@ -145,6 +147,7 @@ constexpr size_t kStageMaxRecords = 131072;  // 2,048 wave chunks: one per resid
 constexpr size_t kStageFirstRecords = 65536;  // 1,024 wave chunks: half the device in dense blocks
 constexpr size_t kCopyPiece = 1 << 20;       // bytes per copy-pool job item
 constexpr size_t kCopyPoolMin = 2 << 20;     // chunks below this many bytes are copied by the calling thread alone
+constexpr size_t kCopyBatch = 8;             // copy pieces between two polls of the pending chunk's uploads
 struct ChunkLaunch {  // a staged chunk's launch: where its parts are on the device, where its verdict words go
   uint8_t* d = nullptr;
   size_t sig = 0, off = 0, msg = 0, mb = 0, c = 0;
@@ -157,6 +160,29 @@ struct StageSlot {
   size_t host_cap = 0;
   hsa_signal_t uploaded{0};  // the slot's DMA uploads: set to their count, each decrements it as it completes
 };
+// The staged form (test hook AT2V_TEST_STAGED=1, a context without a sender cache, a shard part above small_batch_max):
+// ONE launch of the persistent grid over the shard's whole part, issued before any record is uploaded; the records go up
+// in regions of 2^ushift records (>= 65,536, at most kMaxStageRegions) through the same slots and DMA uploads, and the
+// host publishes each landed region in a pinned word the waves poll (at2v_cache.h StagedArgs). Correct (the parity tests
+// run it), but slower than the chunk launches: 12.4-14.9 ms per 1M records against 11.0-11.7 (profiles/r06o-r06v). The
+// device's clock follows its activity: a launch after 1 ms idle takes 10.5 ms instead of 9.6 (6 ms idle: 11.0, r06u),
+// and a grid whose waves sleep while they wait for regions looks idle; chunk launches start only when their records are
+// up. Kept behind the hook for that measurement.
+struct StagedCtl {
+  unsigned long long ready;  // (epoch << 32) | regions published; bit 31 of the count: abort
+  uint32_t timeout;          // set by a wave that gave up waiting
+};
+struct StagedPlan {  // one shard's part of a host-buffer call in the staged form
+  bool active = false;
+  size_t m = 0, lo = 0;  // records, first record (absolute)
+  uint32_t ushift = 16, nreg = 0, submitted = 0, published = 0;
+  std::vector<size_t> at;  // region offsets in the pipe's arena
+  int slot_region[3] = {-1, -1, -1};
+  at2v::StagedArgs args{};
+  bool launched = false;
+};
+constexpr size_t kStageRegionMinLog2 = 16;
+
 struct HostPipe {
   hipStream_t copy = nullptr;                 // the verdict download, (sharded) the all-gathers
   hipStream_t comp[2] = {nullptr, nullptr};   // verify launches of the chunks, alternating
@@ -168,6 +194,8 @@ struct HostPipe {
   bool pending = false;  // a chunk whose uploads are submitted and whose launch is not issued yet
   ChunkLaunch pend;
   uint64_t chunks = 0;  // chunks issued by this shard (slot chunks % kStageSlots, compute stream chunks % 2)
+  StagedCtl* ctl = nullptr;  // pinned, fine-grained (the staged form)
+  uint32_t epoch = 0;
 };
 
 struct Shard {
@@ -183,6 +211,7 @@ struct Shard {
   DevBuf scratch[4];
   DevBuf part[4];  // per scratch set: the classify kernel's hit / miss lists (partitioned cached launches)
   DevBuf btab, pk, sig, msg, off, verdict;
+  const int4* btab24 = nullptr;  // the throughput ladder's 24-bit fixed-base tables, shared per device (bcomb_acquire)
   hipEvent_t copied = nullptr;  // at2v_verify_batch: the verdict copy (the call waits for this, not for the builds)
   SenderCache* cache = nullptr;
   HostPipe* pipe = nullptr;     // the host-buffer path's streams and staging (created by the first host-buffer call)
@@ -207,6 +236,10 @@ struct at2v_ctx {
   size_t stage_first = kStageFirstRecords, stage_max = kStageMaxRecords;
   unsigned copy_threads = 8;
   int pipe_streams = 1;     // create_comp_stream mode (test hook AT2V_TEST_PIPE_STREAMS)
+  bool staged = false;      // test hook AT2V_TEST_STAGED=1: the staged form where it applies (not faster, see StagedCtl)
+  uint32_t stage_nap = 2;   // StagedArgs.nap (test hook AT2V_TEST_STAGE_NAP)
+  uint32_t stage_launch_at = 0;  // test hook AT2V_TEST_STAGE_LAUNCH_AT: the launch once this many regions are published
+  bool stage_pre = false;   // test hook AT2V_TEST_STAGE_PRE: every region uploaded before the launch (kernel-only time)
   bool pipe_trace = false;  // test hook AT2V_TEST_PIPE_TRACE: per host-buffer call, where the host's time went (stderr)
   double tr_wait = 0, tr_copy = 0, tr_enq = 0;  // seconds, this call
   uint64_t host_chunks = 0;  // chunks staged by host-buffer calls (at2v_info.host_chunks)
@@ -237,6 +270,10 @@ int hip_code(hipError_t e) {
     if (e_ != hipSuccess) return hip_code(e_); \
   } while (0)
 
+constexpr int kLadderKey = -24;  // bcomb_acquire's key for the ladder tables (the combs use their window width)
+hipError_t bcomb_acquire(int device, int bits, hipStream_t st, const int4** out);
+void bcomb_release(const int4* p);
+
 int init_shard(Shard& s, int device) {
   s.device = device;
   AT2V_TRY(hipSetDevice(device));
@@ -259,6 +296,8 @@ int init_shard(Shard& s, int device) {
   AT2V_TRY(s.btab.ensure(at2v::btab_bytes()));
   AT2V_TRY(at2v::launch_build_btab((int4*)s.btab.p, s.stream));
   AT2V_TRY(hipStreamSynchronize(s.stream));
+  // the throughput kernels' 24-bit tables [j]B, [j 2^144]B (2 GB, kernels' AT2V_LADDER_BW), one copy per device
+  if (at2v::ladder_btab_bytes()) AT2V_TRY(bcomb_acquire(device, kLadderKey, s.stream, &s.btab24));
   return AT2V_OK;
 }
 
@@ -267,7 +306,7 @@ bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) &
 // The combs of B, shared by every comb context of the process on a device (round 6, VERDICT r5 "Next" 3): built by the
 // first context that needs one (on its stream, synchronously, under the registry's lock: a few ms since they are built by
 // additions), freed with the last. A node's ingest queue and its batch contexts hold one 872 MB + 67 MB pair per device
-// instead of one each.
+// instead of one each. The ladder's 24-bit tables (key kLadderKey, every GPU context) are shared the same way.
 struct SharedBComb {
   int device, bits;
   int4* p;
@@ -289,14 +328,16 @@ hipError_t bcomb_acquire(int device, int bits, hipStream_t st, const int4** out)
     }
   int4* p = nullptr;
   void* scratch = nullptr;
-  hipError_t e = hipMalloc((void**)&p, at2v::bcomb_bytes(bits));
+  const bool ladder = bits == kLadderKey;
+  hipError_t e = hipMalloc((void**)&p, ladder ? at2v::ladder_btab_bytes() : at2v::bcomb_bytes(bits));
   if (e == hipSuccess) e = hipMalloc(&scratch, at2v::bcomb_scratch_bytes());
 #if AT2V_EXP_BCOMB_NOBUILD  // EXPERIMENT (wrong verdicts on the hit path): the hit-list table allocated but never written
-  const bool build = bits == at2v::bcomb_lat_bits();
+  const bool build = ladder || bits == at2v::bcomb_lat_bits();
 #else
   const bool build = true;
 #endif
-  if (e == hipSuccess && build) e = at2v::launch_build_bcomb(p, bits, scratch, st);
+  if (e == hipSuccess && build)
+    e = ladder ? at2v::launch_build_ladder_btab(p, scratch, st) : at2v::launch_build_bcomb(p, bits, scratch, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (scratch) (void)hipFree(scratch);
   if (e != hipSuccess) {
@@ -498,7 +539,7 @@ hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
 // after a compaction waits for it (cache_before_launch). The verdict words are zeroed first (fail closed).
 hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                         uint32_t msg_bytes, const uint32_t* off, uint32_t n, uint32_t* verdicts, hipStream_t stream,
-                        bool zero_verdicts = true, bool pipeline = false) {
+                        bool zero_verdicts = true, bool pipeline = false, const at2v::StagedArgs* staged = nullptr) {
   // a chunk of the host-buffer pipeline whose batch is above small_batch_max: the throughput kernels at every chunk
   // size, with dense grids (launch_verify)
   const uint32_t pair_max = pipeline ? 0u : ctx->pair_max;
@@ -536,8 +577,8 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   }
   if (e == hipSuccess)
     e = at2v::launch_verify(pk, sig, msg, msg_bytes, off, n, (int)ctx->policy, verdicts, (int4*)s.scratch[j].p,
-                            (const int4*)s.btab.p, s.grid, pair_max, stream, c ? &ca : nullptr,
-                            part ? &pa : nullptr, pipeline ? 1 : 0);
+                            (const int4*)s.btab.p, s.btab24, s.grid, pair_max, stream, c ? &ca : nullptr,
+                            part ? &pa : nullptr, pipeline ? 1 : 0, staged);
   if (e == hipSuccess && c) {
     // claims of this launch -> payloads on the build stream (later launches use them; this one did not wait)
     e = hipEventRecord(c->claims_ready[cs], stream);
@@ -561,6 +602,7 @@ void free_pipe(Shard& s) {
     if (sl.host) (void)hipHostFree(sl.host);
     if (sl.uploaded.handle) (void)hsa_signal_destroy(sl.uploaded);
   }
+  if (p->ctl) (void)hipHostFree(p->ctl);
   p->arena.release();
   for (hipEvent_t ev : p->comp_done)
     if (ev) (void)hipEventDestroy(ev);
@@ -630,6 +672,12 @@ hipError_t ensure_pipe(Shard& s, int mode) {
   }
   for (StageSlot& sl : p->slot)
     if (e == hipSuccess) e = hsa_err(hsa_signal_create(0, 0, nullptr, &sl.uploaded));
+  if (e == hipSuccess)
+    e = hipHostMalloc((void**)&p->ctl, sizeof(StagedCtl), hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) {
+    p->ctl->ready = 0;
+    p->ctl->timeout = 0;
+  }
   if (e != hipSuccess) free_pipe(s);
   return e;
 }
@@ -668,8 +716,10 @@ struct CopyJob {
     for (size_t o = 0; o < count; o += step)
       pieces.push_back({(uint8_t*)(dst + o), (const uint8_t*)(src + o), std::min(step, count - o), base, true});
   }
+  size_t base = 0;  // run_copy: the first piece of the batch the pool is running
   static void run_piece(void* a, size_t i) {
-    const CopyPiece& p = static_cast<CopyJob*>(a)->pieces[i];
+    CopyJob* j = static_cast<CopyJob*>(a);
+    const CopyPiece& p = j->pieces[j->base + i];
     if (!p.offsets) {
       std::memcpy(p.dst, p.src, p.len);
       return;
@@ -685,13 +735,22 @@ struct CopyJob {
 // the shard's device bitmap, zeroed by the launch first). Current device = s.device. Returns after the launch is
 // enqueued; the host waits only for the slot's previous upload (and, when the slot must grow, for its previous launch).
 // Host copy of one job (the copy pool's threads for large ones, the calling thread for small ones).
-void run_copy(at2v::CpuPool* copier, CopyJob& job, size_t bytes) {
-  if (copier && bytes >= kCopyPoolMin) {
-    at2v::pool_run(copier, job.pieces.size(), CopyJob::run_piece, &job);
-  } else {
-    for (size_t i = 0; i < job.pieces.size(); ++i) CopyJob::run_piece(&job, i);
+// The pieces go in batches of kCopyBatch; `between` runs after each batch (issue_chunk: launch the previous chunk as soon
+// as its uploads are done, not only after this whole copy).
+template <class Between>
+void run_copy(at2v::CpuPool* copier, CopyJob& job, size_t bytes, Between&& between) {
+  const size_t np = job.pieces.size();
+  for (job.base = 0; job.base < np; job.base += kCopyBatch) {
+    const size_t cnt = std::min(kCopyBatch, np - job.base);
+    if (copier && bytes >= kCopyPoolMin) {
+      at2v::pool_run(copier, cnt, CopyJob::run_piece, &job);
+    } else {
+      for (size_t i = 0; i < cnt; ++i) CopyJob::run_piece(&job, i);
+    }
+    between();
   }
   job.pieces.clear();
+  job.base = 0;
 }
 
 // device bytes a shard's part of a host batch takes in the pipe's arena: every chunk's layout, 256-aligned
@@ -764,19 +823,27 @@ hipError_t issue_chunk(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, const uin
   auto upload = [&](size_t at, size_t len) {
     return hsa_err(hsa_amd_memory_async_copy(d + at, p.gpu, sl.host + at, p.cpu, len, 0, nullptr, sl.uploaded));
   };
+  // between copy batches: the pending (previous) chunk is launched as soon as its uploads have landed, so the device
+  // does not wait for this chunk's whole host copy (the pipeline's fill: the second chunk's launch)
+  hipError_t ef = hipSuccess;
+  auto poll = [&]() {
+    if (ef == hipSuccess && p.pending && hsa_signal_load_scacquire(p.slot[p.pend.slot].uploaded) == 0)
+      ef = flush_chunk(ctx, s);
+  };
   CopyJob job;
   job.add(sl.host, pk + a * 32, c * 32);
-  run_copy(copier, job, c * 32);
+  run_copy(copier, job, c * 32, poll);
   e = upload(0, c * 32);
   job.add(sl.host + L.sig, sig + a * 64, c * 64);
   job.add_offsets((uint32_t*)(sl.host + L.off), msg_off + a, c + 1, mb0);
-  run_copy(copier, job, c * 68);
+  run_copy(copier, job, c * 68, poll);
   if (e == hipSuccess) e = upload(L.sig, L.msg - L.sig);
   if (mb) {
     job.add(sl.host + L.msg, msg + mb0, mb);
-    run_copy(copier, job, mb);
+    run_copy(copier, job, mb, poll);
     if (e == hipSuccess) e = upload(L.msg, mb);
   }
+  if (e == hipSuccess) e = ef;
   if (e != hipSuccess) {  // (a submit failed: nothing waits for this slot's parts any more; the call fails)
     hsa_signal_store_screlease(sl.uploaded, 0);
     return e;
@@ -795,6 +862,158 @@ hipError_t issue_chunk(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, const uin
     ctx->tr_enq += std::chrono::duration<double>(t3 - t2).count();
   }
   return e;
+}
+
+// ---- the staged form (StagedPlan above) ----
+
+void stage_store(HostPipe& p, uint32_t count) {
+  __atomic_store_n(&p.ctl->ready, ((unsigned long long)p.epoch << 32) | count, __ATOMIC_RELEASE);
+}
+
+// Publish the regions whose uploads have landed, in order: those below `block_below` are waited for, later ones only if
+// already done. An upload error (negative signal) is returned; the caller aborts.
+hipError_t stage_publish(HostPipe& p, StagedPlan& sp, uint32_t block_below) {
+  const uint32_t before = sp.published;
+  hipError_t e = hipSuccess;
+  while (sp.published < sp.submitted) {
+    StageSlot& sl = p.slot[sp.published % kStageSlots];
+    if (sp.published >= block_below && hsa_signal_load_scacquire(sl.uploaded) > 0) break;
+    e = wait_uploads(sl);
+    if (e != hipSuccess) break;
+    ++sp.published;
+  }
+  if (sp.published != before) stage_store(p, sp.published);
+  return e;
+}
+
+// the single launch of a staged call, on comp[0]
+hipError_t stage_launch(at2v_ctx* ctx, Shard& s, StagedPlan& sp) {
+  HostPipe& p = *s.pipe;
+  const at2v::StagedArgs& sa = sp.args;
+  const size_t m = sp.m;
+  hipError_t e = launch_shard(ctx, s, (const uint8_t*)p.arena.p, nullptr, nullptr, 0, nullptr, (uint32_t)m,
+                              (uint32_t*)s.verdict.p, p.comp[0], /*zero_verdicts=*/false, /*pipeline=*/true, &sa);
+  if (e == hipSuccess) e = hipEventRecord(p.comp_done[0], p.comp[0]);
+  if (e != hipSuccess) sp.active = false;  // (nothing launched: nobody waits for the word)
+  sp.launched = e == hipSuccess;
+  return e;
+}
+
+// The call's launch for shard s (current device = s.device): layout of the regions in the arena, then the single launch
+// on comp[0]; its waves wait for the regions the host publishes.
+hipError_t stage_begin(at2v_ctx* ctx, Shard& s, StagedPlan& sp, size_t lo, size_t m, const uint32_t* msg_off) {
+  HostPipe& p = *s.pipe;
+  for (StageSlot& sl : p.slot) (void)wait_uploads(sl);  // (after a failed call, uploads may still write the arena)
+  p.pending = false;
+  sp = StagedPlan{};
+  sp.active = true;
+  sp.lo = lo;
+  sp.m = m;
+  sp.ushift = kStageRegionMinLog2;
+  while (((m + ((size_t)1 << sp.ushift) - 1) >> sp.ushift) > (size_t)at2v::kMaxStageRegions) ++sp.ushift;
+  const size_t U = (size_t)1 << sp.ushift;
+  sp.nreg = (uint32_t)((m + U - 1) / U);
+  at2v::StagedArgs sa{};
+  size_t total = 0;
+  sp.at.resize(sp.nreg);
+  for (uint32_t u = 0; u < sp.nreg; ++u) {
+    const size_t a = lo + u * U, c = std::min(U, m - u * U);
+    const size_t mb = (size_t)(msg_off[a + c] - msg_off[a]);
+    sp.at[u] = total;
+    sa.mb[u] = (uint32_t)mb;
+    total += (chunk_layout(c, mb).total + 255) & ~(size_t)255;
+  }
+  hipError_t e = p.arena.ensure(total);
+  if (e != hipSuccess) return e;
+  for (uint32_t u = 0; u < sp.nreg; ++u) sa.at[u] = sp.at[u];
+  ++p.epoch;
+  p.ctl->timeout = 0;
+  stage_store(p, 0);
+  sa.ready = &p.ctl->ready;
+  sa.timeout = &p.ctl->timeout;
+  sa.epoch = p.epoch;
+  sa.ushift = sp.ushift;
+  sa.nreg = sp.nreg;
+  sa.last_c = (uint32_t)(m - (size_t)(sp.nreg - 1) * U);
+  sa.nap = ctx->stage_nap;
+  sp.args = sa;
+  if (ctx->stage_pre || ctx->stage_launch_at) return hipSuccess;  // (stage_launch later)
+  return stage_launch(ctx, s, sp);
+}
+
+// Region u of the plan: host copy into its slot (after the slot's previous region has landed and been published), DMA
+// uploads into the arena; between copy batches, the regions that have landed are published. Region 0 is published as
+// soon as it lands (the launch's waves are waiting for it).
+hipError_t stage_region(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, StagedPlan& sp, const uint8_t* pk,
+                        const uint8_t* sig, const uint8_t* msg, const uint32_t* msg_off) {
+  HostPipe& p = *s.pipe;
+  const uint32_t u = sp.submitted;
+  const size_t U = (size_t)1 << sp.ushift;
+  const size_t a = sp.lo + u * U, c = std::min(U, sp.m - u * U);
+  const uint32_t mb0 = msg_off[a];
+  const size_t mb = (size_t)(msg_off[a + c] - mb0);
+  const ChunkLayout L = chunk_layout(c, mb);
+  const int k = (int)(u % kStageSlots);
+  StageSlot& sl = p.slot[k];
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  hipError_t e = stage_publish(p, sp, u >= kStageSlots ? u - kStageSlots + 1 : 0);  // the slot's previous region
+  if (e == hipSuccess && sl.host_cap < L.total) {
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.host = nullptr;
+    sl.host_cap = 0;
+    const size_t want = std::max(L.total + L.total / 4, chunk_layout(U, 0).total + U * 128);
+    e = hipHostMalloc((void**)&sl.host, want, hipHostMallocDefault);
+    if (e == hipSuccess) sl.host_cap = want;
+  }
+  if (e != hipSuccess) return e;
+  const auto t1 = clk::now();
+  uint8_t* d = (uint8_t*)p.arena.p + sp.at[u];
+  hsa_signal_store_screlease(sl.uploaded, mb ? 3 : 2);
+  auto upload = [&](size_t at, size_t len) {
+    return hsa_err(hsa_amd_memory_async_copy(d + at, p.gpu, sl.host + at, p.cpu, len, 0, nullptr, sl.uploaded));
+  };
+  hipError_t ep = hipSuccess;
+  auto poll = [&]() {
+    if (ep == hipSuccess) ep = stage_publish(p, sp, 0);
+  };
+  CopyJob job;
+  job.add(sl.host, pk + a * 32, c * 32);
+  run_copy(copier, job, c * 32, poll);
+  e = upload(0, c * 32);
+  job.add(sl.host + L.sig, sig + a * 64, c * 64);
+  job.add_offsets((uint32_t*)(sl.host + L.off), msg_off + a, c + 1, mb0);
+  run_copy(copier, job, c * 68, poll);
+  if (e == hipSuccess) e = upload(L.sig, L.msg - L.sig);
+  if (mb) {
+    job.add(sl.host + L.msg, msg + mb0, mb);
+    run_copy(copier, job, mb, poll);
+    if (e == hipSuccess) e = upload(L.msg, mb);
+  }
+  if (e != hipSuccess) {
+    hsa_signal_store_screlease(sl.uploaded, 0);
+    return e;
+  }
+  sp.submitted = u + 1;
+  sp.slot_region[k] = (int)u;
+  const auto t2 = clk::now();
+  e = ep;
+  const uint32_t la = std::min(ctx->stage_launch_at, sp.nreg);
+  if (e == hipSuccess) e = stage_publish(p, sp, u == 0 ? 1 : (!ctx->stage_pre && u + 1 == la ? la : 0));
+  if (e == hipSuccess && !ctx->stage_pre && !sp.launched && la && sp.published >= la) e = stage_launch(ctx, s, sp);
+  ++p.chunks;
+  ++ctx->host_chunks;
+  if (ctx->pipe_trace) {
+    const auto t3 = clk::now();
+    ctx->tr_wait += std::chrono::duration<double>(t1 - t0).count() + std::chrono::duration<double>(t3 - t2).count();
+    ctx->tr_copy += std::chrono::duration<double>(t2 - t1).count();
+  }
+  return e;
+}
+
+// a failed staged call: the launch's waves stop waiting (their chunks' verdicts are 0; the call reports the error)
+void stage_abort(HostPipe& p, StagedPlan& sp) {
+  if (sp.active) stage_store(p, 0x80000000u);
 }
 
 // The pipe's arena for a shard's part of a call (m records, mb message bytes), before its first chunk: every launch of
@@ -936,6 +1155,10 @@ int at2v_create(const at2v_opts* opts, at2v_ctx** out) {
   c->copy_threads = (unsigned)at2v::test_env_long("AT2V_TEST_COPY_THREADS", 8);
   c->pipe_streams = (int)at2v::test_env_long("AT2V_TEST_PIPE_STREAMS", c->pipe_streams);
   c->pipe_trace = at2v::test_env_long("AT2V_TEST_PIPE_TRACE", 0) != 0;
+  c->staged = at2v::test_env_long("AT2V_TEST_STAGED", 0) != 0;
+  c->stage_nap = (uint32_t)at2v::test_env_long("AT2V_TEST_STAGE_NAP", 2);
+  c->stage_pre = at2v::test_env_long("AT2V_TEST_STAGE_PRE", 0) != 0;
+  c->stage_launch_at = (uint32_t)at2v::test_env_long("AT2V_TEST_STAGE_LAUNCH_AT", 0);
   if (c->stage_first < 64) c->stage_first = 64;
   if (c->stage_max < c->stage_first) c->stage_max = c->stage_first;
   c->pair_max = o.small_batch_max == 0 ? AT2V_SMALL_BATCH_DEFAULT
@@ -1003,6 +1226,7 @@ void at2v_destroy(at2v_ctx* ctx) {
     for (DevBuf& b : s.scratch) b.release();
     for (DevBuf& b : s.part) b.release();
     s.btab.release();
+    bcomb_release(s.btab24);
     s.pk.release();
     s.sig.release();
     s.msg.release();
@@ -1036,8 +1260,11 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
   // pipe, then the chunks of all shards round robin, so every device's pipeline fills early and the copy pool serves
   // them in turn.
   std::vector<ChunkPlan> plan(G);
+  std::vector<StagedPlan> stp(G);
   std::vector<size_t> lo(G);
   std::vector<hipError_t> err(G, hipSuccess);
+  const auto tc0 = std::chrono::steady_clock::now();
+  ctx->tr_wait = ctx->tr_copy = ctx->tr_enq = 0;
   for (size_t g = 0; g < G; ++g) {
     Shard& s = ctx->shards[g];
     const at2v::Range r = at2v::device_range(n, G, g);
@@ -1047,17 +1274,27 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     hipError_t e = hipSetDevice(s.device);
     if (e == hipSuccess) e = s.verdict.ensure(((r.size() + 31) / 32) * 4);
     if (e == hipSuccess) e = ensure_pipe(s, ctx->pipe_streams);
-    if (e == hipSuccess) e = begin_arena(ctx, s, r.size(), (size_t)(msg_off[r.hi] - msg_off[r.lo]));
+    if (e == hipSuccess && ctx->staged && !s.cache && r.size() > ctx->pair_max)
+      e = stage_begin(ctx, s, stp[g], r.lo, r.size(), msg_off);
+    else if (e == hipSuccess)
+      e = begin_arena(ctx, s, r.size(), (size_t)(msg_off[r.hi] - msg_off[r.lo]));
     err[g] = e;
   }
-  const auto tc0 = std::chrono::steady_clock::now();
-  ctx->tr_wait = ctx->tr_copy = ctx->tr_enq = 0;
   for (bool more = true; more;) {
     more = false;
     for (size_t g = 0; g < G; ++g) {
-      ChunkPlan& cp = plan[g];
-      if (cp.done() || err[g] != hipSuccess) continue;
+      if (err[g] != hipSuccess) continue;
       Shard& s = ctx->shards[g];
+      if (stp[g].active) {
+        StagedPlan& sp = stp[g];
+        if (sp.submitted >= sp.nreg) continue;
+        err[g] = hipSetDevice(s.device);
+        if (err[g] == hipSuccess) err[g] = stage_region(ctx, s, copier, sp, pk, sig, msg, msg_off);
+        more = more || sp.submitted < sp.nreg;
+        continue;
+      }
+      ChunkPlan& cp = plan[g];
+      if (cp.done()) continue;
       const size_t at = cp.pos, c = cp.take();
       err[g] = hipSetDevice(s.device);
       if (err[g] == hipSuccess)
@@ -1066,12 +1303,18 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
       more = more || !cp.done();
     }
   }
-  for (size_t g = 0; g < G; ++g) {  // the last chunk of every shard
+  for (size_t g = 0; g < G; ++g) {  // the last chunk of every shard / every staged region published
     Shard& s = ctx->shards[g];
     if (plan[g].m == 0 || !s.pipe) continue;
     hipError_t e = hipSetDevice(s.device);
-    if (e == hipSuccess) e = flush_chunk(ctx, s);
+    if (e == hipSuccess && stp[g].active && err[g] == hipSuccess) {
+      e = stage_publish(*s.pipe, stp[g], stp[g].submitted);
+      if (e == hipSuccess && !stp[g].launched) e = stage_launch(ctx, s, stp[g]);
+    }
+    else if (e == hipSuccess && !stp[g].active)
+      e = flush_chunk(ctx, s);
     if (err[g] == hipSuccess) err[g] = e;
+    if (err[g] != hipSuccess) stage_abort(*s.pipe, stp[g]);
   }
   // the verdict words of each shard, once its last two launches are done (copy stream)
   for (size_t g = 0; g < G; ++g) {
@@ -1093,6 +1336,8 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     Shard& s = ctx->shards[g];
     if (plan[g].m == 0 || err[g] != hipSuccess || hipSetDevice(s.device) != hipSuccess) continue;
     hipError_t e = hipEventSynchronize(s.copied);
+    if (e == hipSuccess && stp[g].active && __atomic_load_n(&s.pipe->ctl->timeout, __ATOMIC_ACQUIRE))
+      e = hipErrorLaunchTimeOut;  // (a wave gave up waiting for a region: its chunks' verdicts are 0)
     if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
   if (ctx->pipe_trace)

@@ -69,6 +69,25 @@ struct PartArgs {
 };
 size_t part_bytes_per_record();
 
+// A host-buffer batch verified by ONE launch while its records are still being uploaded (at2v_api.hip, the staged
+// form of the host pipeline). The shard's records are in nreg regions of 2^ushift records (the last one: last_c), each
+// laid out as chunk_layout (pk | sig | rebased offsets | messages, mb[u] bytes) at at[u] of the device arena. The host
+// publishes how many regions have landed in a pinned word, (epoch << 32) | count (bit 31 of count: abort); a wave
+// entering region u polls it until count > u, then takes a system-scope acquire (HSA: the receiving device's acquire
+// before using DMA-written data). No region's lines are read before it is published, and regions are 256-byte aligned,
+// so no cache holds a line of it from before.
+constexpr int kMaxStageRegions = 64;
+struct StagedArgs {
+  uint64_t at[kMaxStageRegions];  // region offsets in the arena (the launch's restrict arena argument: derived
+                                  // pointers keep its no-alias guarantee, so message loads still move across the
+                                  // kernel's table stores; pointers loaded from memory cost 20%, profiles/r06s)
+  uint32_t mb[kMaxStageRegions];
+  const unsigned long long* ready;  // pinned host word
+  uint32_t* timeout;                // pinned host word: a wave gave up waiting (kStageTimeoutTicks)
+  uint32_t epoch, ushift, nreg, last_c;
+  uint32_t nap;  // s_sleep(8) rounds between two polls
+};
+
 // compaction work buffers (one per device; the alternate tag/entry arrays are swapped in by the host)
 struct CacheCompactArgs {
   unsigned long long* new_tags;

@@ -38,6 +38,10 @@ namespace at2v {
 #if AT2V_VERIFY_HALF && AT2V_BWIN != 16
 #error "the half-size path uses 16-bit fixed-base windows"
 #endif
+#ifndef AT2V_LADDER_BW
+#define AT2V_LADDER_BW 16  // fixed-base window of the throughput ladder kernels (verify_half_fu kBW); 24: two shared 1 GB
+                           // tables, 12 B additions instead of 16: +0.1% (106.05 vs 105.92 M/s, profiles/r06l), not adopted
+#endif
 #ifndef AT2V_INV_GROUP
 #define AT2V_INV_GROUP 2  // chunks whose final inversions share one field inversion (Montgomery's trick)
 #endif
@@ -290,6 +294,7 @@ struct LdsTabB {
 // Fixed-base table [0..2^(kBWin-1)]B (affine Niels, 8 x 16 B per entry: 4.2 MB for 16-bit windows,
 // 67 MB for 20, 1.07 GB for 24) in global memory, read through an LDS-DMA prefetch like the A entries.
 constexpr int kBtabEntries = (1 << (kBWin - 1)) + 1;
+constexpr int kLadderEntries = (1 << 23) + 1;  // entries of each 24-bit ladder table (AT2V_LADDER_BW 24)
 struct DevTabB {
   const int4* base;
   int4* stage;  // this wave's 8 x 1 KiB LDS staging buffer
@@ -743,12 +748,58 @@ __device__ AT2V_INLINE void verdict_or(uint32_t* __restrict__ verdicts, uint32_t
 // instead of 64 consecutive records: with kCache ([j]A tables) the hit list's chunks (every record cached: A's decode and
 // table skipped) and then the miss list's, without it the miss list alone (the comb kernel takes the hits). A record's
 // verdict bit is set by an atomic OR (the lists are in no particular order; the launcher zeroed the words).
-template <bool kCache, bool kComb = false, bool kPart = false>
+// kStaged (StagedArgs, the host pipeline's single launch): record i of region u = i >> ushift is read from the region's
+// own layout once the host has published the region (stage_wait); a wave that cannot get it (abort, time limit) stores
+// zero verdict words for its chunks.
+constexpr unsigned long long kStageTimeoutTicks = 1000000000ull;  // 10 s of the 100 MHz s_memrealtime clock
+
+// lane 0 polls the published region count until it exceeds `need` - 1; returns it (wave-uniform), or 0 on abort / time
+// limit (then *dead)
+__device__ AT2V_INLINE uint32_t stage_wait(const StagedArgs* sp, uint32_t need, int lane, bool& dead) {
+  int got = 0;
+  if (lane == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const unsigned long long v = __hip_atomic_load(sp->ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t cnt = (uint32_t)v;
+      if ((uint32_t)(v >> 32) == sp->epoch) {
+        if (cnt & 0x80000000u) {
+          got = -1;
+          break;
+        }
+        if (cnt >= need) {
+          got = (int)cnt;
+          break;
+        }
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kStageTimeoutTicks) {
+        __hip_atomic_store(sp->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        got = -1;
+        break;
+      }
+      for (uint32_t z = 0; z < sp->nap; ++z) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  got = __builtin_amdgcn_readfirstlane(got);
+#ifndef AT2V_STAGE_FENCE
+#define AT2V_STAGE_FENCE 2  // after every poll: 1 a system-scope acquire, 2 a workgroup-scope one (L1), 0 none
+#endif
+#if AT2V_STAGE_FENCE == 1
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+#elif AT2V_STAGE_FENCE == 2
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
+  dead = got < 0;
+  return got < 0 ? 0u : (uint32_t)got;
+}
+
+template <bool kCache, bool kComb = false, bool kPart = false, bool kStaged = false>
 __device__ AT2V_INLINE void verify_chunks(
     int4* astage, int4* rstage, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy,
     uint32_t* __restrict__ verdicts, int4* __restrict__ scratch, const int4* __restrict__ btab,
-    uint32_t* __restrict__ chunk_queue, const CacheArgs* cp, const PartArgs* pp = nullptr) {
+    const int4* __restrict__ btab24, uint32_t* __restrict__ chunk_queue, const CacheArgs* cp,
+    const PartArgs* pp = nullptr, const StagedArgs* sp = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);  // wave-uniform: the LDS stage addresses live in SGPRs
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
@@ -777,8 +828,14 @@ __device__ AT2V_INLINE void verify_chunks(
   const int4* ident = btab + (size_t)kNumBtabs * kBtabEntries * 8;  // shared identity entry after the B tables
   DevTabA ta{slot, astage + wib * 640, lane, ident};
   DevTabA tr{slot + kTabAGranules, rstage + wib * 640, lane, ident};
+#if AT2V_LADDER_BW == 24  // the shared 24-bit tables [j]B and [j 2^144]B (kLadderEntries each, at2v_api.hip)
+  const DevTabB tb0{btab24, astage + wib * 640, lane};                        // staged where A's entry was
+  const DevTabB tb1{btab24 + (size_t)kLadderEntries * 8, rstage + wib * 640, lane};  // in R's stage
+#else
+  (void)btab24;
   const DevTabB tb0{btab, astage + wib * 640, lane};                      // [j]B, staged where A's entry was
   const DevTabB tb1{btab + (size_t)kBtabEntries * 8, rstage + wib * 640, lane};  // [j 2^128]B, in R's stage
+#endif
   auto wmax = [](int v) { return wave_max_i32(v); };
 #if AT2V_FAIR
   uint32_t* prog_lines = chunk_queue + 16;
@@ -799,6 +856,9 @@ __device__ AT2V_INLINE void verify_chunks(
   constexpr uint32_t kHalf = kWavesPerBlock / 2;
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
                                             : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
+  const uint8_t* const arena = pk;  // kStaged: the launch passes its arena as pk
+  uint32_t known = 0;  // kStaged: regions this wave has seen published
+  bool dead = false;   // kStaged: the regions it waits for will not come
   for (uint32_t c = c_first; c < nchunks;) {
     AT2V_PHASE(0);
 #ifdef AT2V_WAIT_PROBE
@@ -819,6 +879,20 @@ __device__ AT2V_INLINE void verify_chunks(
       i = c * 64 + lane;
       ii = i < n ? i : n - 1;  // tail lanes recompute a real record; their bit is masked
       act = i < n;
+    }
+    int skip = 0;  // kStaged: the chunk's region never came (verdicts 0)
+    if constexpr (kStaged) {  // the chunk's region (wave-uniform: regions are multiples of 64 records)
+      const uint32_t u0 = (c * 64) >> sp->ushift, u = u0 < sp->nreg - 1 ? u0 : sp->nreg - 1;
+      if (u >= known && !dead) known = stage_wait(sp, u + 1, lane, dead);
+      skip = u >= known ? 1 : 0;
+      const uint8_t* b = arena + sp->at[u];
+      const uint32_t rc = u == sp->nreg - 1 ? sp->last_c : 1u << sp->ushift;
+      pk = b;
+      sig = b + (size_t)rc * 32;
+      off = reinterpret_cast<const uint32_t*>(b + (size_t)rc * 96);
+      msg = b + (((size_t)rc * 96 + ((size_t)rc + 1) * 4 + 15) & ~(size_t)15);
+      msg_total = sp->mb[u];
+      ii -= u << sp->ushift;
     }
     uint32_t Rw[8], Sw[8], Aw[8];
     load8(Rw, sig + (size_t)ii * 64);
@@ -885,16 +959,20 @@ __device__ AT2V_INLINE void verify_chunks(
           const DevBCombLat tbc{cc.bcomb_lat, {astage + wib * 640, rstage + wib * 640}, lane};
           good = verify_comb_fu(Rw, Aw, Sw, len, msgword, policy, a_ok, tc, tbc) & act;
         } else {
-          good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & act;
+          good = verify_half_fu<false, AT2V_LADDER_BW>(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) &
+                 act;
         }
       } else {
         DevTabA tc{ta};
         if (all_hit) tc.base = cc.payload + (size_t)u * kTabAGranules;
-        good = verify_half_fu<true>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace, all_hit, a_ok) &
+        good = verify_half_fu<true, AT2V_LADDER_BW>(Rw, Aw, Sw, len, msgword, policy, tc, tr, tb0, tb1, wmax, pace,
+                                                     all_hit, a_ok) &
                act;
       }
+    } else if (skip) {
+      good = 0;
     } else {
-      good = verify_half_fu(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & act;
+      good = verify_half_fu<false, AT2V_LADDER_BW>(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & act;
     }
 #else
     const int good = verify_half(Rw, Aw, Sw, len, msgword, policy, ta, tr, tb0, tb1, wmax, pace) & (i < n);
@@ -939,21 +1017,39 @@ __device__ AT2V_INLINE void verify_chunks(
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int4* __restrict__ btab24,
+    uint32_t* __restrict__ chunk_queue) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
-  verify_chunks<false>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue,
-                       nullptr);
+  verify_chunks<false>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, btab24,
+                       chunk_queue, nullptr);
 }
 
 // the same with the per-sender A cache (at2v_opts.sender_cache, tables [j]A)
+// the host pipeline's single launch over a batch still being uploaded (StagedArgs)
+__global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_staged(
+    const uint8_t* __restrict__ arena, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int4* __restrict__ btab24,
+    uint32_t* __restrict__ chunk_queue, StagedArgs sa) {
+  __shared__ int4 astage[kWavesPerBlock * 10 * 64];
+  __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
+  // one system-scope acquire per block before any wave reads a region: no cache keeps a line of the arena from an
+  // earlier launch (the regions are re-uploaded at the same addresses every call)
+  if (threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+  verify_chunks<false, false, false, true>(astage, rstage, arena, arena, arena, 0, nullptr, n, policy, verdicts,
+                                           scratch, btab, btab24, chunk_queue, nullptr, nullptr, &sa);
+}
+
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_cached(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, CacheArgs c) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int4* __restrict__ btab24,
+    uint32_t* __restrict__ chunk_queue, CacheArgs c) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
-  verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, &c);
+  verify_chunks<true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, btab24,
+                      chunk_queue, &c);
 }
 
 // Partitioned cached launches (at2v_cache.h PartArgs): the ladder over the classify kernel's miss list (sender_comb: the
@@ -961,21 +1057,22 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_miss(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, PartArgs p) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int4* __restrict__ btab24,
+    uint32_t* __restrict__ chunk_queue, PartArgs p) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   verify_chunks<false, false, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
-                                    chunk_queue, nullptr, &p);
+                                    btab24, chunk_queue, nullptr, &p);
 }
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel_tables_part(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue, CacheArgs c,
-    PartArgs p) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int4* __restrict__ btab24,
+    uint32_t* __restrict__ chunk_queue, CacheArgs c, PartArgs p) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 rstage[kWavesPerBlock * 10 * 64];
   verify_chunks<true, false, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
-                                   chunk_queue, &c, &p);
+                                   btab24, chunk_queue, &c, &p);
 }
 
 // The classify kernel of a partitioned cached launch: one record per lane, a wave takes kClassifyGroups consecutive
@@ -1791,7 +1888,8 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 #elif AT2V_COMB_PAIRS
   verify_chunks_comb2(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, chunk_queue, c);
 #else
-  verify_chunks<true, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab,
+  static_assert(AT2V_LADDER_BW == 16, "the one-record-per-lane comb kernel keeps the 16-bit fixed-base tables");
+  verify_chunks<true, true>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch, btab, btab,
                             chunk_queue, &c);
 #endif
 }
@@ -2075,7 +2173,8 @@ __global__ __launch_bounds__(kPairBlock, 1) void verify_pair_kernel(
 __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_kernel(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
-    int4* __restrict__ scratch, const int4* __restrict__ btab, uint32_t* __restrict__ chunk_queue) {
+    int4* __restrict__ scratch, const int4* __restrict__ btab, const int4* __restrict__ btab24,
+    uint32_t* __restrict__ chunk_queue) {
   __shared__ int4 astage[kWavesPerBlock * 10 * 64];
   __shared__ int4 bstage[kWavesPerBlock * 8 * 64];
   const int lane = threadIdx.x & 63;
@@ -2611,7 +2710,7 @@ constexpr int kBCombKLog2 = 6;
 constexpr int kBCombK = 1 << kBCombKLog2;       // entries per fill lane
 constexpr uint32_t kBCombFillLanes = 1u << 16;  // lanes per fill launch
 
-__global__ __launch_bounds__(64) void bcomb_base_kernel(gu_cached* __restrict__ base, int bits, int npos) {
+__global__ __launch_bounds__(64) void bcomb_base_kernel(gu_cached* __restrict__ base, int pos_bits, int npos) {
   const int p = threadIdx.x;
   if (p >= npos) return;
   const uint32_t Bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
@@ -2620,9 +2719,9 @@ __global__ __launch_bounds__(64) void bcomb_base_kernel(gu_cached* __restrict__ 
   (void)gu_frombytes(P, Bw);
   gu_p2 Q2;
   gu_p1p1 t;
-  const int nd = bits * p;
+  const int nd = pos_bits * p;
 #pragma unroll 1
-  for (int d = 0; d < nd; ++d) {  // P = [2^(W p)]B
+  for (int d = 0; d < nd; ++d) {  // P = [2^(pos_bits p)]B
     gu_p3_to_p2(Q2, P);
     gu_p2_dbl(t, Q2);
     gu_p1p1_to_p3(P, t);
@@ -2757,11 +2856,12 @@ int bcomb_wide_bits() { return kBCombBits; }
 
 size_t bcomb_scratch_bytes() { return sizeof(gu_cached) * 2 * 16; }
 
-hipError_t launch_build_bcomb(int4* out, int bits, void* scratch, hipStream_t stream) {
-  if (bits != 16 && bits != 20 && bits != 24) return hipErrorInvalidValue;
-  const int npos = (254 + bits - 1) / bits;
+// npos tables of 2^(bits-1) + 1 entries, table p = [j 2^(pos_bits p)]B: the combs of B (pos_bits = bits, every position
+// of a 254-bit scalar) or the ladder's 24-bit fixed-base tables (bits 24, npos 2, pos_bits 144)
+hipError_t launch_build_btables(int4* out, int bits, int npos, int pos_bits, void* scratch, hipStream_t stream) {
+  if ((bits != 16 && bits != 20 && bits != 24) || npos < 1 || npos > 16) return hipErrorInvalidValue;
   gu_cached* base = static_cast<gu_cached*>(scratch);
-  hipLaunchKernelGGL(bcomb_base_kernel, dim3(1), dim3(64), 0, stream, base, bits, npos);
+  hipLaunchKernelGGL(bcomb_base_kernel, dim3(1), dim3(64), 0, stream, base, pos_bits, npos);
   hipError_t e = hipGetLastError();
   const uint32_t lanes = ((1u << (bits - 1)) >> kBCombKLog2) * (uint32_t)npos;
   for (uint32_t l0 = 0; l0 < lanes && e == hipSuccess; l0 += kBCombFillLanes) {
@@ -2770,6 +2870,15 @@ hipError_t launch_build_bcomb(int4* out, int bits, void* scratch, hipStream_t st
     e = hipGetLastError();
   }
   return e;
+}
+
+hipError_t launch_build_bcomb(int4* out, int bits, void* scratch, hipStream_t stream) {
+  return launch_build_btables(out, bits, (254 + bits - 1) / bits, bits, scratch, stream);
+}
+
+size_t ladder_btab_bytes() { return AT2V_LADDER_BW == 24 ? (size_t)2 * kLadderEntries * 128 : 0; }
+hipError_t launch_build_ladder_btab(int4* out, void* scratch, hipStream_t stream) {
+  return launch_build_btables(out, 24, 2, 144, scratch, stream);
 }
 int cache_ctl_words() { return kCtlWords; }
 
@@ -2841,8 +2950,8 @@ size_t part_bytes_per_record() { return 12; }  // hidx, hinfo, midx
 
 hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_total,
                          const uint32_t* off, uint32_t n, int policy, uint32_t* verdicts, int4* scratch,
-                         const int4* btab, int grid, uint32_t pair_max, hipStream_t stream, const CacheArgs* cache,
-                         const PartArgs* part, int dense) {
+                         const int4* btab, const int4* btab24, int grid, uint32_t pair_max, hipStream_t stream,
+                         const CacheArgs* cache, const PartArgs* part, int dense, const StagedArgs* staged) {
   if (n == 0) return hipSuccess;
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
   if (n <= pair_max && !(cache && cache->comb)) {  // (with combs, small batches take the comb kernel: faster still)
@@ -2874,6 +2983,16 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
     if (me != hipSuccess) return me;
   }
 #if AT2V_VERIFY_HALF && AT2V_FIELD_FU
+  if (staged) {  // the whole persistent grid: the records arrive while it runs
+    if (cache) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(verify_kernel_staged, dim3(grid), dim3(kBlock), 0, stream, pk, n, policy, verdicts, scratch,
+                       btab, btab24, queue, *staged);
+    return hipGetLastError();
+  }
+#else
+  if (staged) return hipErrorInvalidValue;
+#endif
+#if AT2V_VERIFY_HALF && AT2V_FIELD_FU
   if (cache && part && n > pair_max) {
     // partitioned (at2v_cache.h PartArgs): classify -> (combs) hit list by comb additions -> ladder over the rest. The
     // control words after the lane slots: [0] the ladder's chunk queue, [1] the comb kernel's, [4..5] the list sizes.
@@ -2890,10 +3009,10 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
       hipLaunchKernelGGL(verify_kernel_comb_part, dim3(g2), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n,
                          policy, verdicts, scratch, btab, queue + 1, *cache, pa);
       hipLaunchKernelGGL(verify_kernel_miss, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                         verdicts, scratch, btab, queue, pa);
+                         verdicts, scratch, btab, btab24, queue, pa);
     } else {
       hipLaunchKernelGGL(verify_kernel_tables_part, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n,
-                         policy, verdicts, scratch, btab, queue, *cache, pa);
+                         policy, verdicts, scratch, btab, btab24, queue, *cache, pa);
     }
     return hipGetLastError();
   }
@@ -2917,12 +3036,12 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
       return hipGetLastError();
     }
     hipLaunchKernelGGL(verify_kernel_cached, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                       verdicts, scratch, btab, queue, *cache);
+                       verdicts, scratch, btab, btab24, queue, *cache);
     return hipGetLastError();
   }
 #endif
   hipLaunchKernelGGL(verify_kernel, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
-                     verdicts, scratch, btab, queue);
+                     verdicts, scratch, btab, btab24, queue);
   return hipGetLastError();
 }
 

@@ -93,7 +93,12 @@ AT2V_HD AT2V_INLINE void build_a_table_from(const gu_p3& P1, TabP& tp) {
   }
 }
 
-template <bool kCacheable = false, class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax,
+// kBW: width of the fixed-base windows. 16 (tb0 = [j]B, tb1 = [j 2^128]B, j <= 2^15, 4.2 MB each: the CPU backend, and
+// the GPU kernels' default until round 6): 8 B windows, at ladder windows 0, 4, ..., 28, each adding two entries. 24
+// (tb0 = [j]B, tb1 = [j 2^144]B, j <= 2^23, 1 GB each, shared per device: the throughput kernels since round 6,
+// AT2V_LADDER_BW): t = sum e_k 2^(24 k), k = 0..10, 6 B windows at ladder windows 0, 6, ..., 30 adding e_k and e_(k+6):
+// 12 mixed additions instead of 16 per verify (-28 M of 1195 M, 1.6% of the MACs), read at random from 2 GB.
+template <bool kCacheable = false, int kBW = 16, class TabP, class TabB0, class TabB1, class MsgWord, class WaveMax,
           class Pace = NoPace>
 AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8], const uint32_t Sw[8], uint32_t len,
                                        MsgWord msgword, int policy, TabP& ta, TabP& tr, const TabB0& tb0,
@@ -190,16 +195,25 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   pace.mark(3);
   uint32_t t[8];
   sc_mul_signed(t, hs, Sw);
-  uint32_t c0d[8], c1d[8], td[8];
+  static_assert(kBW == 16 || kBW == 24, "fixed-base window");
+  constexpr int kTdWords = kBW == 16 ? 8 : 12;  // 24: 11 digits + a zero digit (stored 2^23) for the 12th entry
+  uint32_t c0d[8], c1d[8], td[kTdWords];
   sc_recode4_hi8(c0d, hs.c0);
   sc_recode4_hi8(c1d, hs.c1);
-  sc_recode16(td, t);
+  if constexpr (kBW == 16) {
+    sc_recode16(td, t);
+  } else {
+    sc_recode_w<24>(td, t);
+    td[11] = 1u << 23;
+  }
   // 64 signed radix-16 digits hold values < 2^255 (the reduction keeps max(|c0|, |c1|) < 2^253); a lane
   // that would need a 65th window fails closed
   ok &= hs.bits <= 255;
   const int nw_lane = ok ? hs.bits / 4 + 1 : 0;
   int nw = wave_max(nw_lane);
-  nw = nw < 30 ? 30 : nw;  // B digits sit at windows 0, 4, ..., 28: the top window (no B digit) must lie above them
+  // B digits sit at windows 0, 4, ..., 28 (kBW 16) or 0, 6, ..., 30 (24): the top window (no B digit) lies above them
+  constexpr int kNwMin = kBW == 16 ? 30 : 32;
+  nw = nw < kNwMin ? kNwMin : nw;
   AT2V_PHASE(2);
   pace.mark(1);
 
@@ -336,7 +350,8 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
   uint32_t wa = sel8(c0d, (nw - 2) >> 3), wr = sel8(c1d, (nw - 2) >> 3);
 #endif
   for (int i = nw - 2; i >= 0; --i) {
-    const bool bwin = (i & 3) == 0 && i < 32;
+    const int bk = kBW == 16 ? i >> 2 : i / 6;  // the B digit index of a B window
+    const bool bwin = kBW == 16 ? (i & 3) == 0 && i < 32 : bk * 6 == i && i < 36;
     int e0 = 0, e1 = 0;
 #if AT2V_DIGIT_AHEAD
     // before the pacing store/load of this window: the wait for wa/wr must not wait for them
@@ -351,7 +366,9 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     pace.window();
     wa = sel8(c0d, (i - 1) >> 3);  // i = 0: index -1 selects word 0, unused
     wr = sel8(c1d, (i - 1) >> 3);
-    const uint32_t wt0 = sel8(td, i >> 3), wt1 = sel8(td, 4 + (i >> 3));  // used only when bwin (i < 32)
+    // used only when bwin: kBW 16, the words holding digits i/4 and 8 + i/4; 24, digits i/6 and 6 + i/6 themselves
+    const uint32_t wt0 = kBW == 16 ? sel8(td, i >> 3) : seln<kTdWords>(td, bk);
+    const uint32_t wt1 = kBW == 16 ? sel8(td, 4 + (i >> 3)) : seln<kTdWords>(td, 6 + bk);
 #else
     pace.window();
     const int da = digit4(c0d, i), dr = digit4(c1d, i);
@@ -365,11 +382,17 @@ AT2V_HD AT2V_INLINE int verify_half_fu(const uint32_t Rw[8], const uint32_t Aw[8
     gu_p2_dbl(tt, R2);
     gu_p1p1_to_p3(R3, tt);
     AT2V_PROBE(pace.probe[1], pace.mid());
-    if (bwin) {  // -t digits j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B)
+    if (bwin) {  // -t digits: j = i/4 (table [j]B) and 8 + i/4 (table [j 2^128]B); kBW 24: i/6 and 6 + i/6
 #if AT2V_DIGIT_AHEAD
-      e0 = (1 << 15) - (int)((wt0 >> (16 * ((i >> 2) & 1))) & 0xffff);
-      e1 = (1 << 15) - (int)((wt1 >> (16 * ((i >> 2) & 1))) & 0xffff);
+      if constexpr (kBW == 16) {
+        e0 = (1 << 15) - (int)((wt0 >> (16 * ((i >> 2) & 1))) & 0xffff);
+        e1 = (1 << 15) - (int)((wt1 >> (16 * ((i >> 2) & 1))) & 0xffff);
+      } else {
+        e0 = (1 << 23) - (int)wt0;
+        e1 = (1 << 23) - (int)wt1;
+      }
 #else
+      static_assert(kBW == 16, "the 24-bit fixed-base windows read their digits ahead");
       e0 = (1 << 15) - (int)((sel8(td, i >> 3) >> (16 * ((i >> 2) & 1))) & 0xffff);
       e1 = (1 << 15) - (int)((sel8(td, 4 + (i >> 3)) >> (16 * ((i >> 2) & 1))) & 0xffff);
 #endif

@@ -293,19 +293,21 @@ def test_config3_total_size_on_one_gpu(at2v_mod):
         v.close()
 
 
-# ---- the host-buffer path's chunked pipeline (at2v_api.hip HostPipe; round 6) ----
-# Default context: the first chunk is 32,832 records (one more wave chunk than the low-latency kernel takes), later ones
-# double up to 131,072, and a remainder below the first chunk's size joins the chunk before it. Sizes: one chunk with an
-# absorbed 1-record tail, two chunks (the second ragged), and five chunks (every staging slot reused, the last chunk
-# ragged).
-@pytest.mark.parametrize("streams", ["plain", "priority", "cumask"])
+# ---- the host-buffer path's pipeline (at2v_api.hip HostPipe; round 6) ----
+# The staged form (test hook AT2V_TEST_STAGED=1): one launch over the shard's part, records uploaded in regions of 65,536
+# that the waves wait for. Sizes: one region (32,833 records), two (the second ragged), seven (every staging slot reused).
+# The chunked form (the default): the first chunks are 65,536 records,
+# later ones 131,072, and a remainder below the first chunk's size joins the chunk before it; its two compute streams
+# are created each way (AT2V_TEST_PIPE_STREAMS: one hardware queue or two, so consecutive launches overlap or not).
+@pytest.mark.parametrize("form", ["staged", "chunked-plain", "chunked-priority", "chunked-cumask"])
 @pytest.mark.parametrize("n", [32_833, 98_437, 400_009])
-def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, monkeypatch, n, streams):
-    """at2v_verify_batch through the chunked pipeline (16,384 records, doubling to 131,072, dense grids; 1..6 chunks,
-    every staging slot reused), with its two compute streams created each way (test hook AT2V_TEST_PIPE_STREAMS: on one
-    hardware queue or two, so consecutive chunk launches overlap or not). Adversarial records, record by record against
-    the oracle; a sentinel word after the bitmap stays untouched and the pad bits of the last word are 0"""
-    monkeypatch.setenv("AT2V_TEST_PIPE_STREAMS", {"plain": "0", "priority": "1", "cumask": "2"}[streams])
+def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, monkeypatch, n, form):
+    """at2v_verify_batch through each form of the pipeline. Adversarial records, record by record against the oracle,
+    twice through one context (the second call reuses its staging slots and device arena); a sentinel word after the
+    bitmap stays untouched and the pad bits of the last word are 0"""
+    monkeypatch.setenv("AT2V_TEST_STAGED", "1" if form == "staged" else "0")
+    streams = form.split("-")[-1]
+    monkeypatch.setenv("AT2V_TEST_PIPE_STREAMS", {"staged": "1", "plain": "0", "priority": "1", "cumask": "2"}[streams])
     pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 101, 0, n, 72)
     want = oracle.verify_batch(pk, sig, msg, off)
     lib = at2v_mod.load_library()
@@ -320,6 +322,50 @@ def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, monkeypatch, n, stre
             assert np.array_equal(got, want), (rep, _mismatch(got, want, cls))
             if n % 32:
                 assert int(words[(n - 1) // 32]) >> (n % 32) == 0
+
+
+def test_host_pipeline_staged_alternating_batches(at2v_mod, monkeypatch):
+    """The staged form reads each region as soon as the host publishes it, from DMA-written device memory the previous
+    call's launch also read (same arena, same addresses). Two batches of 1,000,003 records (16 regions, the last one
+    ragged) alternate through one context six times: A every record valid, B the same with an S byte flipped in 5,000
+    records. Any stale line of the other batch would flip verdicts: exactly B's mutated records are rejected each time,
+    and the pad bits stay 0"""
+    import torch
+    n, L = 1_000_003, 100
+    with at2v_mod.BatchVerifier() as g:
+        s = torch.cuda.current_stream().cuda_stream
+        d_pk = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+        d_msg = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+        d_off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+        g.gen_records_device(CFG_SEED + 131, 0, n, L, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                             d_off.data_ptr(), s)
+        torch.cuda.synchronize()
+        pk = d_pk.cpu().numpy()
+        sig_a = d_sig.cpu().numpy().reshape(n, 64).copy()
+        msg = d_msg.cpu().numpy()
+        off = d_off.cpu().numpy().view(np.uint32)
+    rng = np.random.default_rng(20261019)
+    idx = np.sort(rng.choice(n, 5000, replace=False))
+    sig_b = sig_a.copy()
+    sig_b[idx, 32 + rng.integers(0, 31, idx.size)] ^= 0x04
+    lib = at2v_mod.load_library()
+    monkeypatch.setenv("AT2V_TEST_STAGED", "1")
+    with at2v_mod.BatchVerifier() as v:
+        for rep in range(6):
+            sig = sig_b if rep % 2 else sig_a
+            words = np.full((n + 31) // 32 + 1, 0xA5A5A5A5, np.uint32)
+            rc = lib.at2v_verify_batch(v._h, pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, off.ctypes.data, n,
+                                       words.ctypes.data)
+            assert rc == 0
+            assert words[-1] == 0xA5A5A5A5
+            ok = at2v_mod.unpack_verdicts(words[:-1], n)
+            bad = np.nonzero(~ok)[0]
+            if rep % 2:
+                assert np.array_equal(bad, idx), (rep, bad.size)
+            else:
+                assert bad.size == 0, (rep, bad[:10])
+            assert int(words[(n - 1) // 32]) >> (n % 32) == 0
 
 
 def test_host_pipeline_ragged_messages_regrow(at2v_mod, oracle):

@@ -4,7 +4,7 @@ variants, for tuning the HostPipe staging (at2v_api.hip). Each variant sets the 
 AT2V_TEST_STAGE_MAX / AT2V_TEST_COPY_THREADS (AT2V_TEST_HOOKS=1) before creating its context; variants alternate over
 `--rounds` rounds so box drift hits them alike. Also prints the device-API kernel time of the same batch and a
 single-thread numpy copy rate of the batch (host memory bandwidth).
-usage: python tools/abi_probe.py [--n 1048576] [--calls 8] [--rounds 2] [--variants first:max:threads[:streams[:stream]],...]
+usage: python tools/abi_probe.py [--n 1048576] [--calls 8] [--rounds 2] [--variants first:max:threads[:streams[:staged]],...]
 -> one JSON line"""
 import argparse
 import json
@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--msg-len", type=int, default=100)
     ap.add_argument("--variants", default="32768:131072:8")
+    ap.add_argument("--host-only", action="store_true", help="skip the device-API timings (for kernel traces)")
+    ap.add_argument("--lib", default="", help="a libat2v variant (tools/build_variant.sh) instead of the product")
     a = ap.parse_args()
     os.environ["AT2V_TEST_HOOKS"] = "1"
     if "--trace" in sys.argv[1:] or os.environ.get("ABI_PROBE_TRACE"):
@@ -32,6 +34,8 @@ def main():
 
     import at2v
 
+    if a.lib:
+        at2v.load_library(a.lib)
     n, L = a.n, a.msg_len
     dev = "cuda:0"
     g = at2v.BatchVerifier()
@@ -57,7 +61,7 @@ def main():
     # launches may overlap): what chunking a batch into launches costs without any host work
     subs = {}
     ls = at2v.launch_streams(2)
-    for sub in (65536, 131072, 262144, 524288):
+    for sub in () if a.host_only else (65536, 131072, 262144, 524288):
         for nst in (1, 2):
             e0.record(ls[0])
             ls[1].wait_event(e0)
@@ -76,22 +80,37 @@ def main():
     # cold records: four distinct 1M batches (800 MB, beyond the 256 MB MALL) verified round robin, against the same
     # batch re-verified (the headline bench's case: its 200 MB stay MALL-resident)
     cold = []
-    for b in range(4):
+    for b in range(0 if a.host_only else 4):
         bufs = [torch.empty(n * 32, dtype=torch.uint8, device=dev), torch.empty(n * 64, dtype=torch.uint8, device=dev),
                 torch.empty(n * L, dtype=torch.uint8, device=dev), torch.empty(n + 1, dtype=torch.int32, device=dev)]
         g.gen_records_device(0x4154325F, (b + 1) * n, n, L, *(x.data_ptr() for x in bufs), s)
         cold.append(bufs)
     torch.cuda.synchronize()
     e0.record()
-    for k in range(8):
+    for k in range(8 if cold else 0):
         b = cold[k % 4]
         g.verify_batch_device(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), n * L, b[3].data_ptr(), n,
                               d_ver.data_ptr(), s)
     e1.record()
     torch.cuda.synchronize()
-    cold_ms = e0.elapsed_time(e1) / 8
+    cold_ms = e0.elapsed_time(e1) / 8 if cold else 0.0
     del cold
     print(f"[abi_probe] device-API kernel: hot {kernel_ms:.3f} ms, cold {cold_ms:.3f} ms", file=sys.stderr, flush=True)
+    # the same launch after the device sat idle (a host-buffer call's copies leave it so between calls): clock ramp
+    gaps = {}
+    for gap_ms in (0.0, 1.0, 3.0, 6.0):
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            time.sleep(gap_ms / 1e3)
+            e0.record()
+            g.verify_batch_device(d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n * L, d_off.data_ptr(), n,
+                                  d_ver.data_ptr(), s)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        gaps[gap_ms] = sorted(ts)[2]
+    print(f"[abi_probe] device-API kernel after an idle gap (ms -> ms): {gaps}", file=sys.stderr, flush=True)
     pk, sig, msg = d_pk.cpu().numpy(), d_sig.cpu().numpy(), d_msg.cpu().numpy()
     off = d_off.cpu().numpy().view(np.uint32)
     g.close()
@@ -101,12 +120,12 @@ def main():
     np.copyto(tmp, src)
     copy_gbs = src.nbytes / (time.perf_counter() - t0) / 1e9
     words = np.zeros(n // 32 + 1, np.uint32)
-    out = {"n": n, "kernel_ms_device_api": kernel_ms, "kernel_ms_device_api_cold": cold_ms, "device_api_split_ms": subs, "numpy_copy_gbs_1thread": copy_gbs, "variants": {}}
+    out = {"n": n, "kernel_ms_after_gap": gaps, "kernel_ms_device_api": kernel_ms, "kernel_ms_device_api_cold": cold_ms, "device_api_split_ms": subs, "numpy_copy_gbs_1thread": copy_gbs, "variants": {}}
     for r in range(a.rounds):
         for var in a.variants.split(","):
-            first, mx, th, ps, sm = (var.split(":") + ["0", "0"])[:5]
+            first, mx, th, ps, st = (var.split(":") + ["1", "0"])[:5]
             os.environ["AT2V_TEST_PIPE_STREAMS"] = ps
-            os.environ["AT2V_TEST_STREAM"] = sm  # 1: the streaming launch, 0: the chunked pipeline
+            os.environ["AT2V_TEST_STAGED"] = st  # 1: the staged single launch, 0: chunk launches
             os.environ["AT2V_TEST_STAGE_FIRST"] = first
             os.environ["AT2V_TEST_STAGE_MAX"] = mx
             os.environ["AT2V_TEST_COPY_THREADS"] = th

@@ -10,6 +10,6 @@ O=$R/at2-node_amd/at2v/variants
 mkdir -p $O
 make -s -C $R/at2-node_amd >/dev/null
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function "$@" -c $C/at2v_kernels.hip -o $O/k_$TAG.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread $O/k_$TAG.o $C/at2v_api.o $C/at2v_host.o $C/at2v_cpu.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -o $O/libat2v_$TAG.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread $O/k_$TAG.o $C/at2v_api.o $C/at2v_host.o $C/at2v_cpu.o -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib -o $O/libat2v_$TAG.so
 rm -f $O/k_$TAG.o
 echo $O/libat2v_$TAG.so
