@@ -140,7 +140,7 @@ constexpr int kScratchSets = 2;
 // The host refills a pinned slot once its upload is done (`uploaded`, host wait). The first two chunks are half a device
 // each (the pipeline's fill: nothing runs until the first is up), later ones kStageMaxRecords, one full round of the
 // persistent grid. Splitting a batch into such launches costs nothing on the device (1M records as 8 launches of 131,072:
-// 9.30 ms on two streams against 9.34 ms for one launch, profiles/r06j). Round 1 measured the previous form of this call
+// 9.30 ms on two streams against 9.34 ms for one launch, profiles/r06/r06j). Round 1 measured the previous form of this call
 // (pageable hipMemcpyAsync, then verify, then D2H) at 54 M/s against a 78 M/s kernel; the stages were serial.
 constexpr int kStageSlots = 3;
 constexpr size_t kStageMaxRecords = 131072;  // 2,048 wave chunks: one per resident wave of the persistent grid
@@ -164,8 +164,8 @@ struct StageSlot {
 // ONE launch of the persistent grid over the shard's whole part, issued before any record is uploaded; the records go up
 // in regions of 2^ushift records (>= 65,536, at most kMaxStageRegions) through the same slots and DMA uploads, and the
 // host publishes each landed region in a pinned word the waves poll (at2v_cache.h StagedArgs). Correct (the parity tests
-// run it), but slower than the chunk launches: 12.4-14.9 ms per 1M records against 11.0-11.7 (profiles/r06o-r06v). The
-// device's clock follows its activity: a launch after 1 ms idle takes 10.5 ms instead of 9.6 (6 ms idle: 11.0, r06u),
+// run it), but slower than the chunk launches: 12.4-14.9 ms per 1M records against 11.0-11.7 (profiles/r06/r06o-r06v). The
+// device's clock follows its activity: a launch after 1 ms idle takes 10.5 ms instead of 9.6 (6 ms idle: 11.0, profiles/r06/r06u),
 // and a grid whose waves sleep while they wait for regions looks idle; chunk launches start only when their records are
 // up. Kept behind the hook for that measurement.
 struct StagedCtl {
@@ -625,7 +625,7 @@ hsa_status_t find_cpu_agent(hsa_agent_t a, void* data) {
 
 // A compute stream of the pipe. The two must sit on different hardware queues, or their launches run one after the
 // other and every chunk pays its own end-of-launch drain: HIP maps streams onto GPU_MAX_HW_QUEUES (4) shared queues, and
-// in a process with a few streams already the two new ones landed on the same queue (profiles/r06d: queue 4 for both).
+// in a process with a few streams already the two new ones landed on the same queue (profiles/r06/r06d: queue 4 for both).
 // mode 0: plain streams; 1: the second one at the highest priority (a queue of its own priority level); 2: streams with
 // a full CU mask (HIP gives a CU-masked stream a queue of its own). Test hook AT2V_TEST_PIPE_STREAMS.
 hipError_t create_comp_stream(hipStream_t* st, int j, int mode, int device) {
@@ -658,7 +658,7 @@ hipError_t ensure_pipe(Shard& s, int mode) {
   }
   // The uploads go to the DMA engines through HSA directly (a host-to-device hsa_amd_memory_async_copy runs on an SDMA
   // engine): HIP's hipMemcpyAsync handed some of them to blit kernels, which take CUs from the running verify launches
-  // and delay the next one (profiles/r06k, r06m: 1.25 ms for a 13 MB upload beside a launch, against 0.23 ms on SDMA).
+  // and delay the next one (profiles/r06/r06k, r06m: 1.25 ms for a 13 MB upload beside a launch, against 0.23 ms on SDMA).
   // HIP already initialised the runtime; hsa_init only takes a reference.
   if (e == hipSuccess) e = hsa_err(hsa_init());
   if (e == hipSuccess) {

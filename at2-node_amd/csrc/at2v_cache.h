@@ -78,9 +78,8 @@ size_t part_bytes_per_record();
 // so no cache holds a line of it from before.
 constexpr int kMaxStageRegions = 64;
 struct StagedArgs {
-  uint64_t at[kMaxStageRegions];  // region offsets in the arena (the launch's restrict arena argument: derived
-                                  // pointers keep its no-alias guarantee, so message loads still move across the
-                                  // kernel's table stores; pointers loaded from memory cost 20%, profiles/r06s)
+  uint64_t at[kMaxStageRegions];  // region offsets in the launch's arena argument (pointers derived from a restrict
+                                  // kernel argument keep its no-alias guarantee)
   uint32_t mb[kMaxStageRegions];
   const unsigned long long* ready;  // pinned host word
   uint32_t* timeout;                // pinned host word: a wave gave up waiting (kStageTimeoutTicks)

@@ -40,7 +40,7 @@ namespace at2v {
 #endif
 #ifndef AT2V_LADDER_BW
 #define AT2V_LADDER_BW 16  // fixed-base window of the throughput ladder kernels (verify_half_fu kBW); 24: two shared 1 GB
-                           // tables, 12 B additions instead of 16: +0.1% (106.05 vs 105.92 M/s, profiles/r06l), not adopted
+                           // tables, 12 B additions instead of 16: +0.1% (106.05 vs 105.92 M/s, profiles/r06/r06l), not adopted
 #endif
 #ifndef AT2V_INV_GROUP
 #define AT2V_INV_GROUP 2  // chunks whose final inversions share one field inversion (Montgomery's trick)
@@ -2969,7 +2969,7 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   // Blocks: a launch below the full grid spreads its chunks over twice as many blocks, half filled (one wave per SIMD:
   // the lowest latency for a lone batch); `dense` (the host-buffer pipeline's chunk launches, at2v_api.hip HostPipe)
   // fills every block, so a small launch takes few whole CUs at full rate and leaves the rest to the launch beside it
-  // (1M records as 16 launches of 65,536: 13.3 ms half filled, one stream; profiles/r06i)
+  // (1M records as 16 launches of 65,536: 13.3 ms half filled, one stream; profiles/r06/r06i)
   const uint32_t per_block = dense ? kWavesPerBlock : kWavesPerBlock / 2;
   const uint32_t need_blocks = (nchunks + per_block - 1) / per_block;
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);

@@ -752,9 +752,10 @@ def abi_host_leg(args, v, d_pk, d_sig, d_msg, d_off, n, L, headline):
                         "vs_headline": rate / headline, "verdicts_ok": ok,
                         "method": "at2v_verify_batch (the library's synchronous host-buffer entry point) on pageable "
                                   "numpy arrays, one call per batch, back to back; inside: chunked pinned staging "
-                                  "(32,832 then doubling to 131,072 records), copy-pool threads, DMA uploads on a "
-                                  "copy stream, verify launches alternating over two streams, verdict words "
-                                  "downloaded at the end of the call"}}
+                                  "(65,536 records twice, then 131,072), copy-pool threads, SDMA uploads through HSA, "
+                                  "each chunk launched once its uploads landed, launches alternating over two "
+                                  "streams on their own hardware queues, verdict words downloaded at the end of the "
+                                  "call"}}
 
 
 def _pmc_pass(args, n, L, counters):
