@@ -590,12 +590,13 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
 
 // ---- the host-buffer path: chunked, pipelined staging (HostPipe above) ----
 
+hipError_t wait_uploads(StageSlot& sl);
+
 void free_pipe(Shard& s) {
   HostPipe* p = s.pipe;
   if (!p) return;
   for (StageSlot& sl : p->slot)  // (uploads still in flight: a call that failed between submit and launch)
-    if (sl.uploaded.handle)
-      (void)hsa_signal_wait_scacquire(sl.uploaded, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    if (sl.uploaded.handle) (void)wait_uploads(sl);
   for (hipStream_t st : {p->copy, p->comp[0], p->comp[1]})
     if (st) (void)hipStreamSynchronize(st);
   for (StageSlot& sl : p->slot) {
@@ -759,10 +760,19 @@ size_t arena_bytes(size_t m, size_t mb, size_t first) {
   return m * 100 + mb + chunks * (16 + 4 + 16 + 256) + 256;
 }
 
-// wait for a slot's uploads (an SDMA error leaves the signal negative)
+// wait for a slot's uploads (an SDMA error leaves the signal negative). Bounded: uploads that have not landed after
+// kUploadWaitS fail the call instead of hanging it.
+constexpr double kUploadWaitS = 10.0;
 hipError_t wait_uploads(StageSlot& sl) {
-  const hsa_signal_value_t v =
-      hsa_signal_wait_scacquire(sl.uploaded, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+  static const uint64_t hint = [] {  // ~1 ms in HSA timestamp ticks (the wait below re-checks the deadline)
+    uint64_t f = 0;
+    return hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f ? f / 1000 : 100000;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
+  hsa_signal_value_t v;
+  while ((v = hsa_signal_wait_scacquire(sl.uploaded, HSA_SIGNAL_CONDITION_LT, 1, hint, HSA_WAIT_STATE_ACTIVE)) > 0)
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kUploadWaitS)
+      return hipErrorLaunchTimeOut;
   if (v == 0) return hipSuccess;
   hsa_signal_store_screlease(sl.uploaded, 0);  // (reported once; the slot starts clean for the next call)
   return hipErrorUnknown;

@@ -85,6 +85,11 @@ constexpr int kLaneGranules = kTabAGranules + kParkGranules + kPrefGranules;
 constexpr int kNumBtabs = 1;
 #endif
 constexpr size_t kScratchPerWave = (size_t)kLaneGranules * 64 * 16;
+#ifndef AT2V_EXP_COMB3
+#define AT2V_EXP_COMB3 0  // EXPERIMENT ONLY (wrong verdicts): the hit-list comb kernel in 768-thread blocks at three waves per
+                          // SIMD (<= 168 VGPRs), each wave's two LDS stages aliased onto one 10 KB region (VERDICT r5 "Next" 5)
+#endif
+constexpr int kWavesAlloc = AT2V_EXP_COMB3 ? 12 : kWavesPerBlock;  // lane-slot sets per block of the scratch buffer
 
 // A value the compiler cannot prove wave-uniform but that is (the wave index in the block): as an SGPR, the LDS-DMA
 // destinations (M0) need no v_readfirstlane per load. AT2V_WIB_UNIFORM=0: plain VGPR (A/B).
@@ -1903,7 +1908,7 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
 #ifndef AT2V_COMB_MSG_STAGE
 #define AT2V_COMB_MSG_STAGE 1  // messages staged in LDS before SHA-512 (comb2_point_staged); 0: read word by word
 #endif
-template <int kRecs, int kBW>
+template <int kRecs, int kBW, int kWaves = kWavesPerBlock>
 __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const uint8_t* __restrict__ pk,
                                              const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                              uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n,
@@ -1914,8 +1919,8 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
   static_assert(8 * kRecs + 3 * (kRecs / 2) <= kLaneGranules, "the slot holds the parked points and pair inverses");
   const int lane = threadIdx.x & 63;
   const int wib = AT2V_UNIFORM(threadIdx.x >> 6);
-  const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t wave = blockIdx.x * kWaves + wib;
+  const uint32_t nwaves = gridDim.x * kWaves;
   constexpr uint32_t kChunk = 64 * kRecs;
   const uint32_t nchunks = (nh + kChunk - 1) / kChunk;
   const int4* __restrict__ comb = cc.payload;
@@ -1925,7 +1930,7 @@ __device__ AT2V_INLINE void verify_comb_hits(int4* astage, int4* rstage, const u
   int4* const sr = rstage + wib * 640;
   // the context's wide comb of B (AT2V_CTX_BCOMB_WIDE, 24-bit windows: five additions fewer) or the 16-bit one
   const DevBCombW<kBW> tbc{kBW == kBCombLatBits ? cc.bcomb_lat : cc.bcomb, {sa, sr}, lane};
-  constexpr uint32_t kHalf = kWavesPerBlock / 2;
+  constexpr uint32_t kHalf = kWaves / 2;
   const uint32_t c_first = wib < (int)kHalf ? blockIdx.x * kHalf + wib
                                             : gridDim.x * kHalf + blockIdx.x * kHalf + (wib - kHalf);
   auto zload = [&](fu& z, int q) { slot_load(reinterpret_cast<int32_t*>(z.v), slot + 8 * q + 5, 10); };
@@ -2101,6 +2106,22 @@ __global__ __launch_bounds__(kBlock, AT2V_VERIFY_WAVES_PER_SIMD) void verify_ker
     verify_comb_hits<4, kBCombMidBits>(astage, rstage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
                                        chunk_queue, c, p, nh);
 }
+
+#if AT2V_EXP_COMB3
+__global__ __launch_bounds__(768, 3) void verify_kernel_comb_part3(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    uint32_t msg_total, const uint32_t* __restrict__ off, uint32_t n, int policy, uint32_t* __restrict__ verdicts,
+    int4* __restrict__ scratch, uint32_t* __restrict__ chunk_queue, CacheArgs c, PartArgs p) {
+  __shared__ int4 stage[12 * 10 * 64];
+  const uint32_t nh = __builtin_amdgcn_readfirstlane(p.counts[0]);
+  if (c.bcomb_bits == kBCombBits)
+    verify_comb_hits<4, kBCombBits, 12>(stage, stage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+                                        chunk_queue, c, p, nh);
+  else
+    verify_comb_hits<4, kBCombMidBits, 12>(stage, stage, pk, sig, msg, msg_total, off, n, policy, verdicts, scratch,
+                                           chunk_queue, c, p, nh);
+}
+#endif
 
 // ---------------------------------------------------------------------------------------------------------------
 // Low-latency verify for small launches: two lanes per record (lane 2r: A side, lane 2r+1: R side,
@@ -2975,7 +2996,7 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   const int g = (int)((uint32_t)grid < need_blocks ? (uint32_t)grid : need_blocks);
   // chunk queue counter: the word after the `grid` blocks' lane slots (scratch_bytes(grid)); the four-wave comb kernel of
   // small batches strides over its chunks and needs none (one dependent memset less on the latency path)
-  uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesPerBlock);
+  uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + (size_t)grid * kScratchPerWave * kWavesAlloc);
   const bool lat_comb = cache && cache->comb && n <= pair_max;
   const bool parted = cache && part && n > pair_max;  // (zeroes its control words itself, below)
   if (!lat_comb && !parted) {
@@ -3006,8 +3027,15 @@ hipError_t launch_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
     if (cache->comb) {
       const uint32_t need2 = ((n + 255) / 256 + kWavesPerBlock / 2 - 1) / (kWavesPerBlock / 2);
       const int g2 = (int)((uint32_t)grid < need2 ? (uint32_t)grid : need2);
+#if AT2V_EXP_COMB3
+      const uint32_t need3 = ((n + 255) / 256 + 11) / 12;
+      hipLaunchKernelGGL(verify_kernel_comb_part3, dim3((uint32_t)grid < need3 ? grid : need3), dim3(768), 0, stream, pk,
+                         sig, msg, msg_total, off, n, policy, verdicts, scratch, queue + 1, *cache, pa);
+      (void)g2;
+#else
       hipLaunchKernelGGL(verify_kernel_comb_part, dim3(g2), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n,
                          policy, verdicts, scratch, btab, queue + 1, *cache, pa);
+#endif
       hipLaunchKernelGGL(verify_kernel_miss, dim3(g), dim3(kBlock), 0, stream, pk, sig, msg, msg_total, off, n, policy,
                          verdicts, scratch, btab, btab24, queue, pa);
     } else {
@@ -3076,7 +3104,7 @@ hipError_t verify_occupancy(int* blocks_per_cu, int* vgprs) {
   return e;
 }
 
-size_t scratch_bytes_per_block() { return kScratchPerWave * kWavesPerBlock; }
+size_t scratch_bytes_per_block() { return kScratchPerWave * kWavesAlloc; }
 // device scratch of a context launching `grid` blocks: their lane slots + the chunk queue counter
 size_t scratch_bytes(int grid) { return (size_t)grid * scratch_bytes_per_block() + kCtlBytes(grid); }
 int block_threads() { return kBlock; }
@@ -3096,6 +3124,9 @@ unsigned kernel_experiments() {
 #endif
 #if AT2V_EXP_CONST_MSG
   m |= AT2V_EXPERIMENT_CONST_MSG;
+#endif
+#if AT2V_EXP_COMB3
+  m |= AT2V_EXPERIMENT_COMB3;
 #endif
   return m;
 }

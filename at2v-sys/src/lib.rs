@@ -109,6 +109,7 @@ pub const AT2V_EXPERIMENT_COMB_HOT: u32 = 2;
 pub const AT2V_EXPERIMENT_SLOT_WAVES: u32 = 4;
 pub const AT2V_EXPERIMENT_CONST_MSG: u32 = 8;
 pub const AT2V_EXPERIMENT_BCOMB_NOBUILD: u32 = 16;
+pub const AT2V_EXPERIMENT_COMB3: u32 = 32;
 
 pub const AT2V_SMALL_BATCH_DEFAULT: u32 = 32768;
 pub const AT2V_SMALL_BATCH_OFF: u32 = 0xffffffff;

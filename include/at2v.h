@@ -107,6 +107,7 @@ enum {
 #define AT2V_EXPERIMENT_SLOT_WAVES 4u    /* waves share per-lane table slots */
 #define AT2V_EXPERIMENT_CONST_MSG 8u     /* message words from registers */
 #define AT2V_EXPERIMENT_BCOMB_NOBUILD 16u /* the hit-list kernel's comb of B left unwritten */
+#define AT2V_EXPERIMENT_COMB3 32u        /* hit-list comb kernel at three waves per SIMD, its two LDS stages aliased */
 
 /* Create / destroy a context. opts may be NULL (device 0, one GPU, DALEK_V1). Replaces nothing in the
  * reference directly: it owns what drop's SystemManager::run(.., num_cpus::get()) workers did
