@@ -235,7 +235,7 @@ struct at2v_ctx {
   // the host-buffer path's chunk schedule (HostPipe; test hooks AT2V_TEST_STAGE_FIRST / _MAX / AT2V_TEST_COPY_THREADS)
   size_t stage_first = kStageFirstRecords, stage_max = kStageMaxRecords;
   unsigned copy_threads = 8;
-  int pipe_streams = 1;     // create_comp_stream mode (test hook AT2V_TEST_PIPE_STREAMS)
+  int pipe_streams = 0;     // create_comp_stream mode (test hook AT2V_TEST_PIPE_STREAMS)
   bool staged = false;      // test hook AT2V_TEST_STAGED=1: the staged form where it applies (not faster, see StagedCtl)
   uint32_t stage_nap = 2;   // StagedArgs.nap (test hook AT2V_TEST_STAGE_NAP)
   uint32_t stage_launch_at = 0;  // test hook AT2V_TEST_STAGE_LAUNCH_AT: the launch once this many regions are published
@@ -624,11 +624,15 @@ hsa_status_t find_cpu_agent(hsa_agent_t a, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
-// A compute stream of the pipe. The two must sit on different hardware queues, or their launches run one after the
+// A compute stream of the pipe. The two should sit on different hardware queues, or their launches run one after the
 // other and every chunk pays its own end-of-launch drain: HIP maps streams onto GPU_MAX_HW_QUEUES (4) shared queues, and
-// in a process with a few streams already the two new ones landed on the same queue (profiles/r06/r06d: queue 4 for both).
-// mode 0: plain streams; 1: the second one at the highest priority (a queue of its own priority level); 2: streams with
-// a full CU mask (HIP gives a CU-masked stream a queue of its own). Test hook AT2V_TEST_PIPE_STREAMS.
+// in a process with a few streams already the two new ones can land on the same queue (profiles/r06/r06d: queue 4 for
+// both). mode 0 (default): plain streams; 1: the second one at the highest priority (a queue of its own priority level);
+// 2: streams with a full CU mask (HIP gives a CU-masked stream a queue of its own). Test hook AT2V_TEST_PIPE_STREAMS.
+// Mode 1 was the default until the end of round 6: the high-priority queues stay with the process after their streams
+// are gone, and other processes on the GPU paid for them. Config 5 with a polluter process, run by a pytest process whose
+// earlier tests had used 8-shard host-buffer contexts: node queue p99 0.72-1.04 ms with mode 1, 0.48-0.60 ms with mode 0
+// (profiles/r06/r06ab, r06ad, r06ae). In a process with few streams the two modes run a 1M-record call alike (r06aa).
 hipError_t create_comp_stream(hipStream_t* st, int j, int mode, int device) {
   if (mode == 1 && j == 1) {
     int least = 0, greatest = 0;

@@ -307,7 +307,7 @@ def test_host_pipeline_chunks_adversarial(at2v_mod, oracle, monkeypatch, n, form
     bitmap stays untouched and the pad bits of the last word are 0"""
     monkeypatch.setenv("AT2V_TEST_STAGED", "1" if form == "staged" else "0")
     streams = form.split("-")[-1]
-    monkeypatch.setenv("AT2V_TEST_PIPE_STREAMS", {"staged": "1", "plain": "0", "priority": "1", "cumask": "2"}[streams])
+    monkeypatch.setenv("AT2V_TEST_PIPE_STREAMS", {"staged": "0", "plain": "0", "priority": "1", "cumask": "2"}[streams])
     pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 101, 0, n, 72)
     want = oracle.verify_batch(pk, sig, msg, off)
     lib = at2v_mod.load_library()
