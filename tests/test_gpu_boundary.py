@@ -330,10 +330,9 @@ def test_config5_mininode_starting_node_does_not_stall_the_others(at2v_mod):
     first-seen senders; 0.3 s into the traffic another process creates what a starting node creates on the GPU (an
     ingest queue with combs: context, B tables, combs of B, cache; tools/mininode.py --late-builder) while the four
     nodes serve. Round 5's comb-of-B launches of up to 68 ms gave serving nodes a p99 of 65.8 ms; built by additions in
-    short launches they must keep the fresh-senders p50 gate (<= 0.4 ms) and a p99 of at most 2.0 ms on every node, 30x
-    below round 5's stall. Measured p99 with the builder: 0.47-0.58 ms on most boxes, 0.77-1.01 ms on one inside the full
-    suite (profiles/r06/r06u, r06w, r06x), against 0.47-0.50 ms without it. (A node process that itself starts late also
-    carries the backlog its inbox collected meanwhile: --late-node, reported in DESIGN §10f, not gated.)"""
+    short launches they must keep the fresh-senders gates: queue p50 <= 0.4 ms, p99 <= 1.0 ms on every node (measured
+    0.49-0.58 ms, profiles/r06/r06u, r06x, r06af). (A node process that itself starts late also carries the backlog its
+    inbox collected meanwhile: --late-node, reported in DESIGN §10g, not gated.)"""
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mininode.py"), "--nodes", "4", "--rate", "20000",
                           "--seconds", "2", "--batch", "1024", "--delay-us", "1000", "--eager", "1", "--comb", "1",
@@ -348,4 +347,4 @@ def test_config5_mininode_starting_node_does_not_stall_the_others(at2v_mod):
     assert all(p["failed"] == 0 and p["rejected"] == r["bad_signatures"] for p in r["per_node"])
     p50 = [p["queue_p50_us"] for p in r["per_node"]]
     p99 = [p["queue_p99_us"] for p in r["per_node"]]
-    assert max(p50) <= 400.0 and max(p99) <= 2000.0, f"queue p50 {p50} / p99 {p99} us per node"
+    assert max(p50) <= 400.0 and max(p99) <= 1000.0, f"queue p50 {p50} / p99 {p99} us per node"
