@@ -754,8 +754,7 @@ def abi_host_leg(args, v, d_pk, d_sig, d_msg, d_off, n, L, headline):
                                   "numpy arrays, one call per batch, back to back; inside: chunked pinned staging "
                                   "(65,536 records twice, then 131,072), copy-pool threads, SDMA uploads through HSA, "
                                   "each chunk launched once its uploads landed, launches alternating over two "
-                                  "streams on their own hardware queues, verdict words downloaded at the end of the "
-                                  "call"}}
+                                  "streams, verdict words downloaded at the end of the call"}}
 
 
 def _pmc_pass(args, n, L, counters):
