@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = ("at2v_abi_version", "at2v_create", "at2v_destroy", "at2v_ver
                     "at2v_verify_one", "at2v_verify_one_policy", "at2v_strerror", "at2v_gen_records_device",
                     "at2v_gen_records_senders_device", "at2v_gen_records_keys_device", "at2v_sign_batch", "at2v_get_info", "at2v_decode_points",
                     "at2v_comm_get_unique_id", "at2v_comm_init_rank", "at2v_verify_shard_gather_device",
-                    "at2v_verify_batch_sharded",
+                    "at2v_verify_batch_sharded", "at2v_verify_batch_submit", "at2v_verify_batch_wait",
                     "at2v_queue_create", "at2v_queue_destroy", "at2v_queue_submit", "at2v_queue_flush",
                     "at2v_queue_poll", "at2v_queue_get_stats", "at2v_queue_reset_latency",
                     "at2v_pack_send_asset",
@@ -118,6 +118,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.at2v_destroy.restype = None
     lib.at2v_verify_batch.argtypes = [P, P, P, P, P, ctypes.c_size_t, P]
     lib.at2v_verify_batch.restype = ctypes.c_int
+    lib.at2v_verify_batch_submit.argtypes = [P, P, P, P, P, ctypes.c_size_t, P, ctypes.POINTER(ctypes.c_uint64)]
+    lib.at2v_verify_batch_submit.restype = ctypes.c_int
+    lib.at2v_verify_batch_wait.argtypes = [P, ctypes.c_uint64]
+    lib.at2v_verify_batch_wait.restype = ctypes.c_int
     lib.at2v_verify_batch_device.argtypes = [P, P, P, P, ctypes.c_size_t, P, ctypes.c_size_t, P, P]
     lib.at2v_verify_batch_device.restype = ctypes.c_int
     lib.at2v_verify_one.argtypes = [P, P, P, ctypes.c_size_t]
@@ -211,6 +215,14 @@ def launch_streams(count: int = 2, device: Optional[int] = None) -> list:
     return out
 
 
+class PendingBatch:
+    """A submitted host-buffer batch (BatchVerifier.submit_batch): its ticket, verdict words and the arrays the library
+    reads until the wait."""
+
+    def __init__(self, ticket: int, n: int, words: np.ndarray, refs: tuple):
+        self.ticket, self.n, self.words, self._refs = ticket, n, words, refs
+
+
 class BatchVerifier:
     """Owns an at2v context: one or more gfx950 devices, or (num_gpus=0) the library's CPU batch backend."""
 
@@ -273,6 +285,28 @@ class BatchVerifier:
         _check(self._lib.at2v_verify_batch(self._h, _ptr(pk), _ptr(sig), _ptr(msg_arg), _ptr(msg_off), n,
                                            _ptr(words)), "at2v_verify_batch")
         return unpack_verdicts(words, n)
+
+    def submit_batch(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, msg_off: np.ndarray) -> "PendingBatch":
+        """at2v_verify_batch_submit: stage the batch and enqueue its verification; returns the pending call (it holds
+        the arrays until wait_batch). At most two in flight per context."""
+        pk = np.ascontiguousarray(pk, dtype=np.uint8)
+        sig = np.ascontiguousarray(sig, dtype=np.uint8)
+        msg = np.ascontiguousarray(msg, dtype=np.uint8).reshape(-1)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint32)
+        n = len(msg_off) - 1
+        if pk.size != 32 * n or sig.size != 64 * n:
+            raise ValueError("pk/sig/msg_off sizes disagree")
+        words = np.zeros(max(1, (n + 31) // 32), dtype=np.uint32)
+        msg_arg = msg if msg.size else np.zeros(1, np.uint8)
+        t = ctypes.c_uint64(0)
+        _check(self._lib.at2v_verify_batch_submit(self._h, _ptr(pk), _ptr(sig), _ptr(msg_arg), _ptr(msg_off), n,
+                                                  _ptr(words), ctypes.byref(t)), "at2v_verify_batch_submit")
+        return PendingBatch(t.value, n, words, (pk, sig, msg_arg, msg_off))
+
+    def wait_batch(self, pending: "PendingBatch") -> np.ndarray:
+        """at2v_verify_batch_wait -> bool[n] verdicts of a submitted batch"""
+        _check(self._lib.at2v_verify_batch_wait(self._h, pending.ticket), "at2v_verify_batch_wait")
+        return unpack_verdicts(pending.words, pending.n)
 
     def verify_batch_device(self, d_pk: int, d_sig: int, d_msg: int, msg_bytes: int, d_off: int, n: int,
                             d_verdicts: int, stream: int = 0) -> None:

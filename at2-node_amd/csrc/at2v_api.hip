@@ -188,8 +188,10 @@ struct HostPipe {
   hipStream_t comp[2] = {nullptr, nullptr};   // verify launches of the chunks, alternating
   hipEvent_t comp_done[2] = {nullptr, nullptr};
   StageSlot slot[kStageSlots];
-  DevBuf arena;         // a call's chunks on the device, each in its own region (arena_at: the next free byte)
+  DevBuf arenas[2];     // a call's chunks on the device, each in its own region (arena_at: the next free byte); one
+  int cur = 0;          // arena per in-flight host-buffer call (HostCall slot `cur`)
   size_t arena_at = 0;
+  DevBuf& arena() { return arenas[cur]; }
   hsa_agent_t gpu{0}, cpu{0};  // the DMA uploads' destination and source agents
   bool pending = false;  // a chunk whose uploads are submitted and whose launch is not issued yet
   ChunkLaunch pend;
@@ -212,12 +214,31 @@ struct Shard {
   DevBuf part[4];  // per scratch set: the classify kernel's hit / miss lists (partitioned cached launches)
   DevBuf btab, pk, sig, msg, off, verdict;
   const int4* btab24 = nullptr;  // the throughput ladder's 24-bit fixed-base tables, shared per device (bcomb_acquire)
-  hipEvent_t copied = nullptr;  // at2v_verify_batch: the verdict copy (the call waits for this, not for the builds)
+  hipEvent_t copied = nullptr;  // the verdict copy of a device-side call (decode, sharded)
+  DevBuf hverdict[2];            // host-buffer calls: the shard's device bitmap per in-flight call (HostCall slot)
+  hipEvent_t hcopied[2] = {nullptr, nullptr};  // ... and its verdict copy (the call waits for this, not for the builds)
   SenderCache* cache = nullptr;
   HostPipe* pipe = nullptr;     // the host-buffer path's streams and staging (created by the first host-buffer call)
 };
 
 }  // namespace
+
+// A host-buffer call in flight (at2v_verify_batch_submit; at2v_verify_batch is submit + wait). Two slots: a context has at
+// most two such calls in flight, each with its own device bitmap and arena per shard; the host stages the second while
+// the first one's launches run, so the device sees no gap between them.
+struct HostCall {
+  bool active = false, done = false;
+  uint64_t ticket = 0;
+  int rc = 0;
+  const uint8_t *pk = nullptr, *sig = nullptr, *msg = nullptr;
+  const uint32_t* msg_off = nullptr;
+  uint32_t* verdicts = nullptr;
+  size_t n = 0;
+  std::vector<hipError_t> err;  // per shard
+  std::vector<size_t> m;        // per shard: records
+  std::vector<char> staged;     // per shard: the staged form (its timeout word is checked)
+  std::chrono::steady_clock::time_point t0;
+};
 
 // verdict words per rank per all-gather round of at2v_verify_batch_sharded (2M records per rank per round)
 constexpr size_t kGatherWindow = 65536;
@@ -253,6 +274,8 @@ struct at2v_ctx {
   DevBuf status;              // one int32: the cross-rank failure flag (at2v_verify_batch_sharded)
   hipEvent_t gather_done = nullptr;  // recorded after every all-gather, on its stream (at2v_destroy waits for it)
   uint64_t gathers = 0;       // all-gathers issued (at2v_info.gathers)
+  HostCall calls[2];          // host-buffer calls in flight (slot = ticket % 2)
+  uint64_t next_ticket = 1;
 };
 
 namespace {
@@ -286,6 +309,7 @@ int init_shard(Shard& s, int device) {
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   AT2V_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+  for (hipEvent_t& ev : s.hcopied) AT2V_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   if (const char* v = at2v::test_env("AT2V_SCRATCH_SETS")) s.sets = std::min(4, std::max(1, std::atoi(v)));
   for (int j = 0; j < s.sets; ++j) {
     AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free[j], hipEventDisableTiming));
@@ -604,7 +628,7 @@ void free_pipe(Shard& s) {
     if (sl.uploaded.handle) (void)hsa_signal_destroy(sl.uploaded);
   }
   if (p->ctl) (void)hipHostFree(p->ctl);
-  p->arena.release();
+  for (DevBuf& b : p->arenas) b.release();
   for (hipEvent_t ev : p->comp_done)
     if (ev) (void)hipEventDestroy(ev);
   for (hipStream_t st : {p->copy, p->comp[0], p->comp[1]})
@@ -817,8 +841,8 @@ hipError_t issue_chunk(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, const uin
   const uint32_t mb0 = msg_off[a];
   const size_t mb = (size_t)(msg_off[a + c] - mb0);
   const ChunkLayout L = chunk_layout(c, mb);
-  if (p.arena_at + L.total > p.arena.cap) return hipErrorInvalidValue;  // (sized by the caller: cannot happen)
-  uint8_t* d = (uint8_t*)p.arena.p + p.arena_at;
+  if (p.arena_at + L.total > p.arena().cap) return hipErrorInvalidValue;  // (sized by the caller: cannot happen)
+  uint8_t* d = (uint8_t*)p.arena().p + p.arena_at;
   p.arena_at += (L.total + 255) & ~(size_t)255;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -905,7 +929,7 @@ hipError_t stage_launch(at2v_ctx* ctx, Shard& s, StagedPlan& sp) {
   HostPipe& p = *s.pipe;
   const at2v::StagedArgs& sa = sp.args;
   const size_t m = sp.m;
-  hipError_t e = launch_shard(ctx, s, (const uint8_t*)p.arena.p, nullptr, nullptr, 0, nullptr, (uint32_t)m,
+  hipError_t e = launch_shard(ctx, s, (const uint8_t*)p.arena().p, nullptr, nullptr, 0, nullptr, (uint32_t)m,
                               (uint32_t*)s.verdict.p, p.comp[0], /*zero_verdicts=*/false, /*pipeline=*/true, &sa);
   if (e == hipSuccess) e = hipEventRecord(p.comp_done[0], p.comp[0]);
   if (e != hipSuccess) sp.active = false;  // (nothing launched: nobody waits for the word)
@@ -937,7 +961,7 @@ hipError_t stage_begin(at2v_ctx* ctx, Shard& s, StagedPlan& sp, size_t lo, size_
     sa.mb[u] = (uint32_t)mb;
     total += (chunk_layout(c, mb).total + 255) & ~(size_t)255;
   }
-  hipError_t e = p.arena.ensure(total);
+  hipError_t e = p.arena().ensure(total);
   if (e != hipSuccess) return e;
   for (uint32_t u = 0; u < sp.nreg; ++u) sa.at[u] = sp.at[u];
   ++p.epoch;
@@ -982,7 +1006,7 @@ hipError_t stage_region(at2v_ctx* ctx, Shard& s, at2v::CpuPool* copier, StagedPl
   }
   if (e != hipSuccess) return e;
   const auto t1 = clk::now();
-  uint8_t* d = (uint8_t*)p.arena.p + sp.at[u];
+  uint8_t* d = (uint8_t*)p.arena().p + sp.at[u];
   hsa_signal_store_screlease(sl.uploaded, mb ? 3 : 2);
   auto upload = [&](size_t at, size_t len) {
     return hsa_err(hsa_amd_memory_async_copy(d + at, p.gpu, sl.host + at, p.cpu, len, 0, nullptr, sl.uploaded));
@@ -1037,7 +1061,7 @@ hipError_t begin_arena(at2v_ctx* ctx, Shard& s, size_t m, size_t mb) {
   for (StageSlot& sl : p.slot) (void)wait_uploads(sl);  // (after a failed call, uploads may still write the arena)
   p.pending = false;
   p.arena_at = 0;
-  return p.arena.ensure(arena_bytes(m, mb, std::min(ctx->stage_first, std::max<size_t>(m, 1))));
+  return p.arena().ensure(arena_bytes(m, mb, std::min(ctx->stage_first, std::max<size_t>(m, 1))));
 }
 
 // The chunk schedule of one shard's part of a host batch: a part the low-latency kernel takes whole (<= small_batch_max
@@ -1235,6 +1259,9 @@ void at2v_destroy(at2v_ctx* ctx) {
     for (hipEvent_t ev : s.scratch_free)
       if (ev) (void)hipEventDestroy(ev);
     if (s.copied) (void)hipEventDestroy(s.copied);
+    for (hipEvent_t ev : s.hcopied)
+      if (ev) (void)hipEventDestroy(ev);
+    for (DevBuf& b : s.hverdict) b.release();
     free_pipe(s);
     free_cache(s.cache);
     for (DevBuf& b : s.scratch) b.release();
@@ -1253,45 +1280,44 @@ void at2v_destroy(at2v_ctx* ctx) {
   delete ctx;
 }
 
-int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                      const uint32_t* msg_off, size_t n, uint32_t* verdicts) {
-  if (!ctx) return AT2V_E_INVALID;
-  if (n == 0) return AT2V_OK;
-  if (!pk || !sig || !msg_off || !verdicts || n >= (1u << 31)) return AT2V_E_INVALID;
-  if (!msg && msg_off[n] != msg_off[0]) return AT2V_E_INVALID;
-  if (!at2v::offsets_valid(msg_off, n)) return AT2V_E_INVALID;  // whole batch, before any device work
-  if (ctx->shards.empty()) {  // CPU context
-    at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
-    ++ctx->cpu_batches;
-    return AT2V_OK;
-  }
-  int prev = 0;
-  (void)hipGetDevice(&prev);
-  const size_t G = ctx->shards.size();
-  int rc = AT2V_OK;
+namespace {
+
+// Issue a host-buffer call into slot k: per shard (64-aligned index range: its words start at word lo/32 of the caller's
+// array) the device bitmap and the pipe, then the chunks of all shards round robin, so every device's pipeline fills
+// early and the copy pool serves them in turn; then the verdict copies. Returns once everything is enqueued (the host
+// copies are done; the launches and downloads run on).
+void host_call_issue(at2v_ctx* ctx, int k) {
+  HostCall& hc = ctx->calls[k];
+  const uint8_t *pk = hc.pk, *sig = hc.sig, *msg = hc.msg;
+  const uint32_t* msg_off = hc.msg_off;
+  const size_t n = hc.n, G = ctx->shards.size();
   at2v::CpuPool* copier = copy_pool(ctx);
-  // Per shard (64-aligned index range: its words start at word lo/32 of the caller's array): the device bitmap and the
-  // pipe, then the chunks of all shards round robin, so every device's pipeline fills early and the copy pool serves
-  // them in turn.
   std::vector<ChunkPlan> plan(G);
   std::vector<StagedPlan> stp(G);
   std::vector<size_t> lo(G);
-  std::vector<hipError_t> err(G, hipSuccess);
-  const auto tc0 = std::chrono::steady_clock::now();
+  std::vector<hipError_t>& err = hc.err;
+  err.assign(G, hipSuccess);
+  hc.m.assign(G, 0);
+  hc.staged.assign(G, 0);
+  hc.t0 = std::chrono::steady_clock::now();
   ctx->tr_wait = ctx->tr_copy = ctx->tr_enq = 0;
   for (size_t g = 0; g < G; ++g) {
     Shard& s = ctx->shards[g];
     const at2v::Range r = at2v::device_range(n, G, g);
     lo[g] = r.lo;
     plan[g].init(r.size(), ctx);
+    hc.m[g] = r.size();
     if (r.size() == 0) continue;
     hipError_t e = hipSetDevice(s.device);
-    if (e == hipSuccess) e = s.verdict.ensure(((r.size() + 31) / 32) * 4);
+    if (e == hipSuccess) e = s.hverdict[k].ensure(((r.size() + 31) / 32) * 4);
     if (e == hipSuccess) e = ensure_pipe(s, ctx->pipe_streams);
-    if (e == hipSuccess && ctx->staged && !s.cache && r.size() > ctx->pair_max)
+    if (e == hipSuccess) s.pipe->cur = k;
+    if (e == hipSuccess && ctx->staged && !s.cache && r.size() > ctx->pair_max) {
       e = stage_begin(ctx, s, stp[g], r.lo, r.size(), msg_off);
-    else if (e == hipSuccess)
+      hc.staged[g] = 1;
+    } else if (e == hipSuccess) {
       e = begin_arena(ctx, s, r.size(), (size_t)(msg_off[r.hi] - msg_off[r.lo]));
+    }
     err[g] = e;
   }
   for (bool more = true; more;) {
@@ -1312,7 +1338,7 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
       const size_t at = cp.pos, c = cp.take();
       err[g] = hipSetDevice(s.device);
       if (err[g] == hipSuccess)
-        err[g] = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, lo[g] + at, c, (uint32_t*)s.verdict.p + at / 32,
+        err[g] = issue_chunk(ctx, s, copier, pk, sig, msg, msg_off, lo[g] + at, c, (uint32_t*)s.hverdict[k].p + at / 32,
                              cp.m > ctx->pair_max, at == 0);
       more = more || !cp.done();
     }
@@ -1324,9 +1350,9 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     if (e == hipSuccess && stp[g].active && err[g] == hipSuccess) {
       e = stage_publish(*s.pipe, stp[g], stp[g].submitted);
       if (e == hipSuccess && !stp[g].launched) e = stage_launch(ctx, s, stp[g]);
-    }
-    else if (e == hipSuccess && !stp[g].active)
+    } else if (e == hipSuccess && !stp[g].active) {
       e = flush_chunk(ctx, s);
+    }
     if (err[g] == hipSuccess) err[g] = e;
     if (err[g] != hipSuccess) stage_abort(*s.pipe, stp[g]);
   }
@@ -1340,24 +1366,34 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
     HostPipe* p = s.pipe;
     for (int j = 0; j < 2 && e == hipSuccess; ++j) e = hipStreamWaitEvent(p->copy, p->comp_done[j], 0);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(verdicts + lo[g] / 32, s.verdict.p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost, p->copy);
-    if (e == hipSuccess) e = hipEventRecord(s.copied, p->copy);
+      e = hipMemcpyAsync(hc.verdicts + lo[g] / 32, s.hverdict[k].p, ((m + 31) / 32) * 4, hipMemcpyDeviceToHost,
+                         p->copy);
+    if (e == hipSuccess) e = hipEventRecord(s.hcopied[k], p->copy);
     err[g] = e;
-    if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
-  // shards run concurrently on their own devices/streams; wait for all of them (not for the cache builds behind them)
-  for (size_t g = 0; g < G; ++g) {
+}
+
+// Complete slot k's call: wait for its verdict copies (not for the cache builds behind them); on a device error with
+// AT2V_CTX_CPU_FALLBACK, drain and verify the batch on the CPU (the caller's buffers are still valid: the call has not
+// returned to the caller as complete).
+void host_call_finish(at2v_ctx* ctx, int k) {
+  HostCall& hc = ctx->calls[k];
+  if (!hc.active || hc.done) return;
+  int rc = AT2V_OK;
+  for (size_t g = 0; g < ctx->shards.size(); ++g)
+    if (hc.m[g] && hc.err[g] != hipSuccess && rc == AT2V_OK) rc = hip_code(hc.err[g]);
+  for (size_t g = 0; g < ctx->shards.size(); ++g) {
     Shard& s = ctx->shards[g];
-    if (plan[g].m == 0 || err[g] != hipSuccess || hipSetDevice(s.device) != hipSuccess) continue;
-    hipError_t e = hipEventSynchronize(s.copied);
-    if (e == hipSuccess && stp[g].active && __atomic_load_n(&s.pipe->ctl->timeout, __ATOMIC_ACQUIRE))
+    if (hc.m[g] == 0 || hc.err[g] != hipSuccess || hipSetDevice(s.device) != hipSuccess) continue;
+    hipError_t e = hipEventSynchronize(s.hcopied[k]);
+    if (e == hipSuccess && hc.staged[g] && __atomic_load_n(&s.pipe->ctl->timeout, __ATOMIC_ACQUIRE))
       e = hipErrorLaunchTimeOut;  // (a wave gave up waiting for a region: its chunks' verdicts are 0)
     if (e != hipSuccess && rc == AT2V_OK) rc = hip_code(e);
   }
   if (ctx->pipe_trace)
-    std::fprintf(stderr, "[at2v pipe] n %zu: %.3f ms (host: wait %.3f, copy %.3f, enqueue %.3f ms)\n", n,
-                 std::chrono::duration<double>(std::chrono::steady_clock::now() - tc0).count() * 1e3, ctx->tr_wait * 1e3,
-                 ctx->tr_copy * 1e3, ctx->tr_enq * 1e3);
+    std::fprintf(stderr, "[at2v pipe] n %zu: %.3f ms (host: wait %.3f, copy %.3f, enqueue %.3f ms)\n", hc.n,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - hc.t0).count() * 1e3,
+                 ctx->tr_wait * 1e3, ctx->tr_copy * 1e3, ctx->tr_enq * 1e3);
   if (rc != AT2V_OK && ctx->cpu) {
     // AT2V_CTX_CPU_FALLBACK: the records are still in the caller's host buffers. Drain what the shards enqueued (no
     // verdict copy of this call may land after the CPU's words), then verify the whole batch on the CPU backend.
@@ -1367,13 +1403,92 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
       if (s.pipe)
         for (hipStream_t st : {s.pipe->copy, s.pipe->comp[0], s.pipe->comp[1]}) (void)hipStreamSynchronize(st);
     }
-    at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
+    at2v::cpu_verify_batch(ctx->cpu, hc.pk, hc.sig, hc.msg, hc.msg_off, hc.n, (int)ctx->policy, hc.verdicts);
     ++ctx->cpu_batches;
     ++ctx->cpu_fallbacks;
     rc = AT2V_OK;
   }
+  hc.rc = rc;
+  hc.done = true;
+}
+
+// complete every host-buffer call still in flight (their results stay for at2v_verify_batch_wait)
+void drain_host_calls(at2v_ctx* ctx) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (uint64_t t = ctx->next_ticket > 2 ? ctx->next_ticket - 2 : 1; t < ctx->next_ticket; ++t)
+    if (ctx->calls[t % 2].ticket == t) host_call_finish(ctx, (int)(t % 2));
   (void)hipSetDevice(prev);
-  return rc;
+}
+
+int host_call_check(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint32_t* msg_off,
+                    size_t n, uint32_t* verdicts) {
+  if (!ctx) return AT2V_E_INVALID;
+  if (n == 0) return AT2V_OK;
+  if (!pk || !sig || !msg_off || !verdicts || n >= (1u << 31)) return AT2V_E_INVALID;
+  if (!msg && msg_off[n] != msg_off[0]) return AT2V_E_INVALID;
+  if (!at2v::offsets_valid(msg_off, n)) return AT2V_E_INVALID;  // whole batch, before any device work
+  return AT2V_OK;
+}
+
+}  // namespace
+
+int at2v_verify_batch_submit(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                             const uint32_t* msg_off, size_t n, uint32_t* verdicts, uint64_t* ticket) {
+  if (!ticket) return AT2V_E_INVALID;
+  *ticket = 0;
+  const int chk = host_call_check(ctx, pk, sig, msg, msg_off, n, verdicts);
+  if (chk != AT2V_OK) return chk;
+  const uint64_t t = ctx->next_ticket++;
+  const int k = (int)(t % 2);
+  HostCall& hc = ctx->calls[k];
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  host_call_finish(ctx, k);  // the call two tickets back: its slot's bitmaps and arenas are reused (its result is lost
+                             // unless waited for; at most two calls are in flight)
+  if (ctx->staged) drain_host_calls(ctx);  // (the staged form's ready word serves one call at a time)
+  hc = HostCall{};
+  hc.active = true;
+  hc.ticket = t;
+  hc.pk = pk;
+  hc.sig = sig;
+  hc.msg = msg;
+  hc.msg_off = msg_off;
+  hc.n = n;
+  hc.verdicts = verdicts;
+  *ticket = t;
+  if (n == 0) {
+    hc.done = true;
+  } else if (ctx->shards.empty()) {  // CPU context: verified now
+    at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
+    ++ctx->cpu_batches;
+    hc.done = true;
+  } else {
+    host_call_issue(ctx, k);
+  }
+  (void)hipSetDevice(prev);
+  return AT2V_OK;
+}
+
+int at2v_verify_batch_wait(at2v_ctx* ctx, uint64_t ticket) {
+  if (!ctx || ticket == 0 || ticket >= ctx->next_ticket) return AT2V_E_INVALID;
+  HostCall& hc = ctx->calls[ticket % 2];
+  if (hc.ticket != ticket || !hc.active) return AT2V_E_INVALID;  // already waited for, or two or more calls back
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  host_call_finish(ctx, (int)(ticket % 2));
+  (void)hipSetDevice(prev);
+  hc.active = false;
+  return hc.rc;
+}
+
+int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                      const uint32_t* msg_off, size_t n, uint32_t* verdicts) {
+  const int chk = host_call_check(ctx, pk, sig, msg, msg_off, n, verdicts);
+  if (chk != AT2V_OK || n == 0) return chk;
+  uint64_t t = 0;
+  const int rc = at2v_verify_batch_submit(ctx, pk, sig, msg, msg_off, n, verdicts, &t);
+  return rc != AT2V_OK ? rc : at2v_verify_batch_wait(ctx, t);
 }
 
 int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
@@ -1486,6 +1601,7 @@ int at2v_verify_batch_sharded(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* s
   if (!ctx || !ctx->comm || n >= (1u << 31)) return AT2V_E_INVALID;
   if (n && (!pk || !sig || !msg_off || !verdicts || (!msg && msg_off[n] != msg_off[0]))) return AT2V_E_INVALID;
   if (n && !at2v::offsets_valid(msg_off, n)) return AT2V_E_INVALID;
+  drain_host_calls(ctx);  // (they share the shard's pipe)
   Shard& s = ctx->shards[0];
   const size_t wpr = at2v::shard_words_per_rank(n, ctx->world);
   const at2v::Range r = at2v::rank_range(n, ctx->world, ctx->rank);

@@ -228,6 +228,9 @@ extern "C" {
     pub fn at2v_destroy(ctx: *mut At2vCtx);
     pub fn at2v_verify_batch(ctx: *mut At2vCtx, pk: *const u8, sig: *const u8, msg: *const u8, msg_off: *const u32,
                              n: usize, verdicts: *mut u32) -> c_int;
+    pub fn at2v_verify_batch_submit(ctx: *mut At2vCtx, pk: *const u8, sig: *const u8, msg: *const u8,
+                                    msg_off: *const u32, n: usize, verdicts: *mut u32, ticket: *mut u64) -> c_int;
+    pub fn at2v_verify_batch_wait(ctx: *mut At2vCtx, ticket: u64) -> c_int;
     pub fn at2v_verify_batch_device(ctx: *mut At2vCtx, d_pk: *const u8, d_sig: *const u8, d_msg: *const u8,
                                     msg_bytes: usize, d_msg_off: *const u32, n: usize, d_verdicts: *mut u32,
                                     hip_stream: *mut c_void) -> c_int;

@@ -26,7 +26,8 @@ extern "C" {
 #endif
 
 /* ABI version of this header. Every struct passed by pointer is copied whole, so adding a field is an ABI break:
- * version 7 appended at2v_info.experiments / host_chunks (and the AT2V_EXPERIMENT_* bits); version 6 appended at2v_opts.cpu_threads / flags (num_gpus = 0 now means the CPU batch backend, no device),
+ * version 7 appended at2v_info.experiments / host_chunks (and the AT2V_EXPERIMENT_* bits) and added
+ * at2v_verify_batch_submit / _wait; version 6 appended at2v_opts.cpu_threads / flags (num_gpus = 0 now means the CPU batch backend, no device),
  * at2v_info.cpu_threads / cpu_batches / cpu_fallbacks / cache_sightings / cache_built / cache_build_us /
  * cache_record_hits,
  * at2v_gen_records_keys_device, at2v_queue_opts.cpu_threads (with the
@@ -128,6 +129,20 @@ void at2v_destroy(at2v_ctx* ctx);
  * The library does not retain any pointer after return. n may be 0. n < 2^31. */
 int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                       const uint32_t* msg_off, size_t n, uint32_t* verdicts);
+
+/* The same call in two halves, so that a caller can stage its next batch while the device verifies this one (the
+ * synchronous call leaves the device idle while it copies its first chunk and after it returns).
+ * at2v_verify_batch_submit validates the batch, copies it to the device and enqueues its launches and its verdict
+ * download, then returns a ticket (> 0). The caller's arrays, verdicts included, must stay valid and unchanged until
+ * at2v_verify_batch_wait(ctx, ticket) has returned; only then are the verdict words final. At most two calls are in
+ * flight per context: a submit completes the call two tickets back first (its verdicts land; its result code is lost
+ * unless it was waited for). Waiting returns that call's result: AT2V_OK, or the error at2v_verify_batch would have
+ * returned (with AT2V_CTX_CPU_FALLBACK the batch is re-verified on the CPU inside the wait). A ticket is waited for
+ * once; an unknown, repeated or too old ticket gives AT2V_E_INVALID. at2v_verify_batch = submit + wait; the other batch
+ * entry points complete the calls in flight first. Validation errors are returned by the submit (no ticket). */
+int at2v_verify_batch_submit(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                             const uint32_t* msg_off, size_t n, uint32_t* verdicts, uint64_t* ticket);
+int at2v_verify_batch_wait(at2v_ctx* ctx, uint64_t ticket);
 
 /* Batch verify on device-resident buffers of ctx's first device (AT2V_E_NODEVICE on a CPU context), asynchronously on
  * `hip_stream`

@@ -96,6 +96,31 @@ def test_cpu_context_decode_points(at2v_mod, cpu_ctx, golden, oracle):
     assert 0 < got.sum() < g.n
 
 
+def test_cpu_context_submit_wait(at2v_mod, golden):
+    """at2v_verify_batch_submit / _wait on a CPU context (the batch is verified inside the submit): tickets count up,
+    each is waited for once, a repeated, unknown or zero ticket is AT2V_E_INVALID, and a submit completes the call two
+    tickets back"""
+    lib = at2v_mod.load_library()
+    with at2v_mod.BatchVerifier(num_gpus=0, cpu_threads=2) as v:
+        a = v.submit_batch(golden["adversarial"].pk, golden["adversarial"].sig, golden["adversarial"].msg,
+                           golden["adversarial"].off)
+        b = v.submit_batch(golden["edge"].pk, golden["edge"].sig, golden["edge"].msg, golden["edge"].off)
+        assert b.ticket == a.ticket + 1
+        assert np.array_equal(v.wait_batch(b), golden["edge"].dalek)
+        assert np.array_equal(v.wait_batch(a), golden["adversarial"].dalek)
+        assert lib.at2v_verify_batch_wait(v._h, a.ticket) == -1  # waited already
+        assert lib.at2v_verify_batch_wait(v._h, 0) == -1
+        assert lib.at2v_verify_batch_wait(v._h, b.ticket + 5) == -1
+        r = golden["rfc8032"]
+        c = v.submit_batch(r.pk, r.sig, r.msg, r.off)
+        d = v.submit_batch(r.pk, r.sig, r.msg, r.off)
+        e = v.submit_batch(r.pk, r.sig, r.msg, r.off)  # completes c (its slot), whose result is then gone
+        assert lib.at2v_verify_batch_wait(v._h, c.ticket) == -1
+        assert np.array_equal(v.wait_batch(d), r.dalek) and np.array_equal(v.wait_batch(e), r.dalek)
+        t = __import__("ctypes").c_uint64(7)
+        assert lib.at2v_verify_batch_submit(v._h, None, None, None, None, 5, None, t) == -1 and t.value == 0
+
+
 def test_cpu_context_counts_batches(at2v_mod, golden):
     g = golden["rfc8032"]
     with at2v_mod.BatchVerifier(num_gpus=0, cpu_threads=2) as v:

@@ -368,6 +368,35 @@ def test_host_pipeline_staged_alternating_batches(at2v_mod, monkeypatch):
             assert int(words[(n - 1) // 32]) >> (n % 32) == 0
 
 
+@pytest.mark.parametrize("shards", [1, 8])
+def test_host_async_submit_wait(at2v_mod, oracle, monkeypatch, shards):
+    """at2v_verify_batch_submit / _wait on the device (one shard, and 8 shards through the alias hook): three batches
+    with two in flight (A and B submitted, A waited, C submitted while B verifies, then B and C), record by record against
+    the oracle; the verdict words of each land in its own array with pad bits 0; a synchronous call between submits
+    completes the call in flight; a repeated ticket is AT2V_E_INVALID"""
+    if shards > 1:
+        monkeypatch.setenv("AT2V_TEST_DEVICE_ALIAS", "1")
+    lib = at2v_mod.load_library()
+    batches = []
+    for k, (n, L) in enumerate(((100_003, 72), (163_841, 100), (40_001, 48))):
+        pk, sig, msg, off, cls = oracle.gen_adversarial(CFG_SEED + 211 + k, 0, n, L)
+        batches.append((pk, sig, msg, off, oracle.verify_batch(pk, sig, msg, off)))
+    with at2v_mod.BatchVerifier(num_gpus=shards) as v:
+        for rep in range(2):
+            a = v.submit_batch(*batches[0][:4])
+            b = v.submit_batch(*batches[1][:4])
+            assert np.array_equal(v.wait_batch(a), batches[0][4])
+            c = v.submit_batch(*batches[2][:4])
+            if rep:  # a synchronous call completes B and C first (their results stay for their waits)
+                assert np.array_equal(v.verify_batch(*batches[0][:4]), batches[0][4])
+            assert np.array_equal(v.wait_batch(b), batches[1][4])
+            assert np.array_equal(v.wait_batch(c), batches[2][4])
+            for p_, bt in ((a, batches[0]), (b, batches[1]), (c, batches[2])):
+                n = len(bt[4])
+                assert int(p_.words[(n - 1) // 32]) >> (n % 32) == 0 if n % 32 else True
+            assert lib.at2v_verify_batch_wait(v._h, b.ticket) == -1
+
+
 def test_host_pipeline_ragged_messages_regrow(at2v_mod, oracle):
     """ragged messages (0 B .. 16 KiB) tiled to 100,000 records at an offset msg_off[0] > 0: the chunks carry very
     different message bytes, so staging slots regrow mid-call; record by record against the oracle"""
