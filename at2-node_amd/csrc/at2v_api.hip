@@ -179,6 +179,7 @@ struct StagedPlan {  // one shard's part of a host-buffer call in the staged for
   std::vector<size_t> at;  // region offsets in the pipe's arena
   int slot_region[3] = {-1, -1, -1};
   at2v::StagedArgs args{};
+  uint32_t* verdicts = nullptr;  // the call's device bitmap for this shard
   bool launched = false;
 };
 constexpr size_t kStageRegionMinLog2 = 16;
@@ -188,8 +189,8 @@ struct HostPipe {
   hipStream_t comp[2] = {nullptr, nullptr};   // verify launches of the chunks, alternating
   hipEvent_t comp_done[2] = {nullptr, nullptr};
   StageSlot slot[kStageSlots];
-  DevBuf arenas[2];     // a call's chunks on the device, each in its own region (arena_at: the next free byte); one
-  int cur = 0;          // arena per in-flight host-buffer call (HostCall slot `cur`)
+  DevBuf arenas[3];     // a call's chunks on the device, each in its own region (arena_at: the next free byte); one
+  int cur = 0;          // arena per host-buffer call slot (HostCall slot `cur`, allocated when first used)
   size_t arena_at = 0;
   DevBuf& arena() { return arenas[cur]; }
   hsa_agent_t gpu{0}, cpu{0};  // the DMA uploads' destination and source agents
@@ -215,17 +216,19 @@ struct Shard {
   DevBuf btab, pk, sig, msg, off, verdict;
   const int4* btab24 = nullptr;  // the throughput ladder's 24-bit fixed-base tables, shared per device (bcomb_acquire)
   hipEvent_t copied = nullptr;  // the verdict copy of a device-side call (decode, sharded)
-  DevBuf hverdict[2];            // host-buffer calls: the shard's device bitmap per in-flight call (HostCall slot)
-  hipEvent_t hcopied[2] = {nullptr, nullptr};  // ... and its verdict copy (the call waits for this, not for the builds)
+  DevBuf hverdict[3];            // host-buffer calls: the shard's device bitmap per call slot (HostCall)
+  hipEvent_t hcopied[3] = {nullptr, nullptr, nullptr};  // ... and its verdict copy (the call waits for this, not for
+                                                        // the cache builds behind it)
   SenderCache* cache = nullptr;
   HostPipe* pipe = nullptr;     // the host-buffer path's streams and staging (created by the first host-buffer call)
 };
 
 }  // namespace
 
-// A host-buffer call in flight (at2v_verify_batch_submit; at2v_verify_batch is submit + wait). Two slots: a context has at
-// most two such calls in flight, each with its own device bitmap and arena per shard; the host stages the second while
-// the first one's launches run, so the device sees no gap between them.
+// A host-buffer call in flight. Slots 0 and 1: at2v_verify_batch_submit (slot = ticket % 2; at most two in flight, each
+// with its own device bitmap and arena per shard, so the host stages the second while the first one's launches run and
+// the device sees no gap between them). Slot 2: the synchronous at2v_verify_batch, after the calls in flight are
+// complete (their results stay for their waits).
 struct HostCall {
   bool active = false, done = false;
   uint64_t ticket = 0;
@@ -274,7 +277,7 @@ struct at2v_ctx {
   DevBuf status;              // one int32: the cross-rank failure flag (at2v_verify_batch_sharded)
   hipEvent_t gather_done = nullptr;  // recorded after every all-gather, on its stream (at2v_destroy waits for it)
   uint64_t gathers = 0;       // all-gathers issued (at2v_info.gathers)
-  HostCall calls[2];          // host-buffer calls in flight (slot = ticket % 2)
+  HostCall calls[3];          // host-buffer call slots (HostCall)
   uint64_t next_ticket = 1;
 };
 
@@ -309,7 +312,7 @@ int init_shard(Shard& s, int device) {
   s.grid = s.cus * s.blocks_per_cu;
   AT2V_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   AT2V_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
-  for (hipEvent_t& ev : s.hcopied) AT2V_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (hipEvent_t& ev : s.hcopied) AT2V_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));  // (3 slots)
   if (const char* v = at2v::test_env("AT2V_SCRATCH_SETS")) s.sets = std::min(4, std::max(1, std::atoi(v)));
   for (int j = 0; j < s.sets; ++j) {
     AT2V_TRY(hipEventCreateWithFlags(&s.scratch_free[j], hipEventDisableTiming));
@@ -556,6 +559,12 @@ hipError_t enqueue_cache_build(SenderCache& c, const PendingBuild& b) {
   return e;
 }
 
+bool scratch_ok(const Shard& s) {
+  for (int j = 0; j < s.sets; ++j)
+    if (!s.scratch[j].p) return false;
+  return s.btab.p != nullptr;
+}
+
 // One verify launch on shard s (current device = s.device), on `stream`. The launch takes the shard's next scratch set
 // and waits for the launch that last used that set, on whatever stream that ran; launches on different streams may
 // therefore run concurrently (on one stream they are ordered anyway). Cached launches may overlap too: they share the tag
@@ -567,6 +576,7 @@ hipError_t launch_shard(at2v_ctx* ctx, Shard& s, const uint8_t* pk, const uint8_
   // a chunk of the host-buffer pipeline whose batch is above small_batch_max: the throughput kernels at every chunk
   // size, with dense grids (launch_verify)
   const uint32_t pair_max = pipeline ? 0u : ctx->pair_max;
+  if (!verdicts || (!pk && !staged) || !scratch_ok(s)) return hipErrorInvalidValue;  // (never launch on a null buffer)
   if (ctx->test_fail_launches) {  // test hook: a launch failure, as a faulting device would report it
     --ctx->test_fail_launches;
     return hipErrorLaunchFailure;
@@ -930,7 +940,7 @@ hipError_t stage_launch(at2v_ctx* ctx, Shard& s, StagedPlan& sp) {
   const at2v::StagedArgs& sa = sp.args;
   const size_t m = sp.m;
   hipError_t e = launch_shard(ctx, s, (const uint8_t*)p.arena().p, nullptr, nullptr, 0, nullptr, (uint32_t)m,
-                              (uint32_t*)s.verdict.p, p.comp[0], /*zero_verdicts=*/false, /*pipeline=*/true, &sa);
+                              sp.verdicts, p.comp[0], /*zero_verdicts=*/false, /*pipeline=*/true, &sa);
   if (e == hipSuccess) e = hipEventRecord(p.comp_done[0], p.comp[0]);
   if (e != hipSuccess) sp.active = false;  // (nothing launched: nobody waits for the word)
   sp.launched = e == hipSuccess;
@@ -939,12 +949,14 @@ hipError_t stage_launch(at2v_ctx* ctx, Shard& s, StagedPlan& sp) {
 
 // The call's launch for shard s (current device = s.device): layout of the regions in the arena, then the single launch
 // on comp[0]; its waves wait for the regions the host publishes.
-hipError_t stage_begin(at2v_ctx* ctx, Shard& s, StagedPlan& sp, size_t lo, size_t m, const uint32_t* msg_off) {
+hipError_t stage_begin(at2v_ctx* ctx, Shard& s, StagedPlan& sp, size_t lo, size_t m, const uint32_t* msg_off,
+                       uint32_t* d_verdicts) {
   HostPipe& p = *s.pipe;
   for (StageSlot& sl : p.slot) (void)wait_uploads(sl);  // (after a failed call, uploads may still write the arena)
   p.pending = false;
   sp = StagedPlan{};
   sp.active = true;
+  sp.verdicts = d_verdicts;
   sp.lo = lo;
   sp.m = m;
   sp.ushift = kStageRegionMinLog2;
@@ -1313,7 +1325,7 @@ void host_call_issue(at2v_ctx* ctx, int k) {
     if (e == hipSuccess) e = ensure_pipe(s, ctx->pipe_streams);
     if (e == hipSuccess) s.pipe->cur = k;
     if (e == hipSuccess && ctx->staged && !s.cache && r.size() > ctx->pair_max) {
-      e = stage_begin(ctx, s, stp[g], r.lo, r.size(), msg_off);
+      e = stage_begin(ctx, s, stp[g], r.lo, r.size(), msg_off, (uint32_t*)s.hverdict[k].p);
       hc.staged[g] = 1;
     } else if (e == hipSuccess) {
       e = begin_arena(ctx, s, r.size(), (size_t)(msg_off[r.hi] - msg_off[r.lo]));
@@ -1486,9 +1498,28 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
                       const uint32_t* msg_off, size_t n, uint32_t* verdicts) {
   const int chk = host_call_check(ctx, pk, sig, msg, msg_off, n, verdicts);
   if (chk != AT2V_OK || n == 0) return chk;
-  uint64_t t = 0;
-  const int rc = at2v_verify_batch_submit(ctx, pk, sig, msg, msg_off, n, verdicts, &t);
-  return rc != AT2V_OK ? rc : at2v_verify_batch_wait(ctx, t);
+  if (ctx->shards.empty()) {  // CPU context
+    at2v::cpu_verify_batch(ctx->cpu, pk, sig, msg, msg_off, n, (int)ctx->policy, verdicts);
+    ++ctx->cpu_batches;
+    return AT2V_OK;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  drain_host_calls(ctx);
+  HostCall& hc = ctx->calls[2];
+  hc = HostCall{};
+  hc.active = true;
+  hc.pk = pk;
+  hc.sig = sig;
+  hc.msg = msg;
+  hc.msg_off = msg_off;
+  hc.n = n;
+  hc.verdicts = verdicts;
+  host_call_issue(ctx, 2);
+  host_call_finish(ctx, 2);
+  hc.active = false;
+  (void)hipSetDevice(prev);
+  return hc.rc;
 }
 
 int at2v_verify_batch_device(at2v_ctx* ctx, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,

@@ -138,8 +138,9 @@ int at2v_verify_batch(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, cons
  * flight per context: a submit completes the call two tickets back first (its verdicts land; its result code is lost
  * unless it was waited for). Waiting returns that call's result: AT2V_OK, or the error at2v_verify_batch would have
  * returned (with AT2V_CTX_CPU_FALLBACK the batch is re-verified on the CPU inside the wait). A ticket is waited for
- * once; an unknown, repeated or too old ticket gives AT2V_E_INVALID. at2v_verify_batch = submit + wait; the other batch
- * entry points complete the calls in flight first. Validation errors are returned by the submit (no ticket). */
+ * once; an unknown, repeated or too old ticket gives AT2V_E_INVALID. at2v_verify_batch and at2v_verify_batch_sharded
+ * complete the calls in flight first (their results stay for their waits). Validation errors are returned by the
+ * submit (no ticket). */
 int at2v_verify_batch_submit(at2v_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                              const uint32_t* msg_off, size_t n, uint32_t* verdicts, uint64_t* ticket);
 int at2v_verify_batch_wait(at2v_ctx* ctx, uint64_t ticket);
